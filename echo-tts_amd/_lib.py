@@ -1,0 +1,91 @@
+"""ctypes binding of the C ABI declared in `include/echo_hip.h`.
+
+This is the only place the shared library is loaded. If `libecho_hip.so` is
+missing the import fails loudly: the product path has no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libecho_hip.so")
+
+ECHO_BF16, ECHO_F32 = 0, 1
+EPI_STORE, EPI_SWIGLU, EPI_RESID, EPI_F32OUT = 0, 1, 2, 3
+ACT_NONE, ACT_SILU = 0, 1
+ERRORS = {-1: "ECHO_EINVAL", -2: "ECHO_EDTYPE", -3: "ECHO_ESHAPE", -4: "ECHO_EALIGN"}
+
+vp, i32, i64, f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [("dtype", i32), ("M", i32), ("N", i32), ("K", i32), ("batch", i32),
+                ("A", vp), ("lda", i64), ("stride_a", i64),
+                ("W", vp), ("ldw", i64), ("stride_w", i64),
+                ("C", vp), ("ldc", i64), ("stride_c", i64),
+                ("bias", vp), ("stride_bias", i64),
+                ("aux", vp), ("ld_aux", i64), ("stride_aux", i64),
+                ("gate", vp), ("stride_gate", i64),
+                ("epilogue", i32), ("act", i32), ("out_div", f32), ("tile", i32)]
+
+
+class KVSegment(C.Structure):
+    _fields_ = [("k", vp), ("v", vp), ("ld_tok", i64), ("ld_batch", i64), ("batch_mod", i32),
+                ("capacity", i32), ("len", vp), ("causal", i32)]
+
+
+class AttnArgs(C.Structure):
+    _fields_ = [("dtype", i32), ("rows", i32), ("n_q", i32), ("heads", i32), ("nseg", i32),
+                ("q", vp), ("q_ld_tok", i64), ("q_ld_batch", i64),
+                ("gate", vp), ("g_ld_tok", i64), ("g_ld_batch", i64),
+                ("out", vp), ("o_ld_tok", i64), ("o_ld_batch", i64),
+                ("scale", f32), ("seg", KVSegment * 4)]
+
+
+class StepArgs(C.Structure):
+    _fields_ = [("has_cfg", i32), ("cfg_text", f32), ("cfg_speaker", f32), ("rescale", i32),
+                ("omt", f32), ("ratio", f32), ("inv_omt", f32), ("dt", f32)]
+
+
+# name -> (restype, argtypes); must match include/echo_hip.h exactly
+SIGNATURES = {
+    "echo_gemm": (i32, [C.POINTER(GemmArgs), vp]),
+    "echo_attention": (i32, [C.POINTER(AttnArgs), vp]),
+    "echo_rmsnorm": (i32, [i32, vp, i64, vp, vp, i64, i32, i32, f32, vp]),
+    "echo_adaln_modulate": (i32, [i32, vp, vp, i32, i32, vp, vp, i32, i64, f32, vp]),
+    "echo_head_norm_rope": (i32, [i32, vp, i64, i32, i32, i32, i64, i64, vp, i64, vp, i32, i32, i32, i32,
+                                  f32, vp]),
+    "echo_timestep_embedding": (i32, [i32, vp, vp, vp, i32, i32, vp]),
+    "echo_silu": (i32, [i32, vp, i64, vp, i64, i32, i32, vp]),
+    "echo_adaln_finish": (i32, [i32, vp, vp, i32, i32, i32, vp]),
+    "echo_latent_to_input": (i32, [i32, vp, vp, i32, i32, i32, i32, vp]),
+    "echo_euler_step": (i32, [vp, vp, i64, C.POINTER(StepArgs), vp]),
+    "echo_embed": (i32, [i32, vp, vp, vp, i32, i32, vp]),
+    "echo_scale_rows": (i32, [i32, vp, i64, i32, i32, f32, vp]),
+    "echo_cast_from_f32": (i32, [i32, vp, vp, i64, vp]),
+    "echo_version": (C.c_char_p, []),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load the library (once) and bind every declared symbol; raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} not found: build it with `python -c 'import __graft_entry__ as g; "
+                           f"g.build()'` (the HIP path has no CPU fallback)")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError if a declared symbol is missing
+        fn.restype, fn.argtypes = res, args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {ERRORS.get(rc, f'hipError {rc}')}")

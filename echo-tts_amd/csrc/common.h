@@ -1,0 +1,82 @@
+// Shared device helpers for the gfx950 kernels: bf16 storage, rounding, vector types.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/echo_hip.h"
+
+typedef uint16_t bf16_t;  // bfloat16 storage (no arithmetic on it)
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+
+__device__ __forceinline__ float bf2f(uint32_t u16) { return __uint_as_float(u16 << 16); }
+
+// Round-to-nearest-even fp32 -> bf16 (hardware v_cvt_pk_bf16_f32; NaN stays NaN).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+__device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
+
+// Element-type traits: rounding points of the reference's dtype contract.
+template <typename T> struct Elt;
+template <> struct Elt<bf16_t> {
+  static __device__ __forceinline__ float ld(const bf16_t* p) { return bf2f(*p); }
+  static __device__ __forceinline__ void st(bf16_t* p, float v) { *p = f2bf(v); }
+  static __device__ __forceinline__ float rnd(float v) { return rbf(v); }
+  static constexpr int bytes = 2;
+};
+template <> struct Elt<float> {
+  static __device__ __forceinline__ float ld(const float* p) { return *p; }
+  static __device__ __forceinline__ void st(float* p, float v) { *p = v; }
+  static __device__ __forceinline__ float rnd(float v) { return v; }
+  static constexpr int bytes = 4;
+};
+
+// Load/store 8 consecutive elements as fp32 (16 B for bf16, 2x16 B for fp32).
+__device__ __forceinline__ void load8(const bf16_t* p, float* o) {
+  uint4 u = *(const uint4*)p;
+  uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { o[2 * i] = bf2f(w[i] & 0xffffu); o[2 * i + 1] = bf2f(w[i] >> 16); }
+}
+__device__ __forceinline__ void load8(const float* p, float* o) {
+  float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float* v) {
+  uint4 u;
+  u.x = pack2bf(v[0], v[1]); u.y = pack2bf(v[2], v[3]); u.z = pack2bf(v[4], v[5]); u.w = pack2bf(v[6], v[7]);
+  *(uint4*)p = u;
+}
+__device__ __forceinline__ void store8(float* p, const float* v) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+// Correctly rounded elementwise helpers that the compiler must not contract.
+__device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
+__device__ __forceinline__ float sigmoid_f(float v) { return 1.0f / (1.0f + expf(-v)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+#define ECHO_LAUNCH_CHECK()                         \
+  do {                                              \
+    hipError_t _e = hipGetLastError();              \
+    if (_e != hipSuccess) return (int)_e;           \
+  } while (0)

@@ -1,0 +1,358 @@
+// elementwise.hip — bandwidth-bound kernels of the sampling path.
+//
+// Every kernel moves 16 B per lane (8 bf16 or 4+4 fp32) and reproduces the
+// reference's rounding points; fp32 arithmetic is kept
+// un-contracted (-ffp-contract=off) so that sequences like `x*s1 + shift`
+// round exactly where the reference rounds.
+#include "common.h"
+
+namespace {
+
+constexpr int NB = 256;  // threads per row block
+
+// Block-wide sum over NB threads (4 waves) via LDS.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+// RMSNorm(x) * w : model.py:99-104. One block per row; dim % 8 == 0, dim <= 8*NB*4.
+template <typename T>
+__global__ void __launch_bounds__(NB) rmsnorm_kernel(const T* __restrict__ x, int64_t ldx,
+                                                     const T* __restrict__ w, T* __restrict__ y,
+                                                     int64_t ldy, int dim, float eps) {
+  __shared__ float red[4];
+  const T* xr = x + blockIdx.x * ldx;
+  T* yr = y + blockIdx.x * ldy;
+  constexpr int MAXC = 4;
+  float v[MAXC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int i = (c * NB + threadIdx.x) * 8;
+    if (i < dim) {
+      load8(xr + i, v[c]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += v[c][e] * v[c][e];
+    }
+  }
+  ss = block_sum(ss, red);
+  const float r = 1.0f / sqrtf(ss / (float)dim + eps);
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int i = (c * NB + threadIdx.x) * 8;
+    if (i < dim) {
+      float wv[8], o[8];
+      load8(w + i, wv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (v[c][e] * r) * wv[e];
+      store8(yr + i, o);
+    }
+  }
+}
+
+// LowRankAdaLN tail: model.py:76-83 (scale1 = round(scale+1) precomputed).
+template <typename T>
+__global__ void __launch_bounds__(NB) adaln_kernel(const T* __restrict__ x, T* __restrict__ y, int dim,
+                                                   const T* __restrict__ shift, const T* __restrict__ scale1,
+                                                   int rows_per_vec, int64_t vec_stride, float eps) {
+  __shared__ float red[4];
+  const T* xr = x + (int64_t)blockIdx.x * dim;
+  T* yr = y + (int64_t)blockIdx.x * dim;
+  const int64_t vo = (int64_t)(blockIdx.x / rows_per_vec) * vec_stride;
+  shift += vo;
+  scale1 += vo;
+  constexpr int MAXC = 4;
+  float v[MAXC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int i = (c * NB + threadIdx.x) * 8;
+    if (i < dim) {
+      load8(xr + i, v[c]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += v[c][e] * v[c][e];
+    }
+  }
+  ss = block_sum(ss, red);
+  const float r = 1.0f / sqrtf(ss / (float)dim + eps);
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int i = (c * NB + threadIdx.x) * 8;
+    if (i < dim) {
+      float s1[8], sh[8], o[8];
+      load8(scale1 + i, s1);
+      load8(shift + i, sh);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = ((v[c][e] * r) * s1[e]) + sh[e];
+      store8(yr + i, o);
+    }
+  }
+}
+
+// Per-head RMSNorm (+RoPE) in place: one wave per (row, 4 heads), 16 lanes per head,
+// 8 elements per lane (RoPE pairs are lane-local).
+template <typename T>
+__global__ void __launch_bounds__(NB) head_norm_rope_kernel(T* __restrict__ x, int64_t ldx, int rows, int heads,
+                                                            int nblk, int64_t col0, int64_t col_stride,
+                                                            const T* __restrict__ w, int64_t w_stride,
+                                                            const float* __restrict__ rope, int rope_heads,
+                                                            int seq_len, int pos0, int pos_mult, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int hg = (heads + 3) / 4;  // head groups of 4 per wave
+  const int64_t task = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t total = (int64_t)rows * nblk * hg;
+  if (task >= total) return;
+  const int grp = task % hg;
+  const int blk = (task / hg) % nblk;
+  const int row = task / ((int64_t)hg * nblk);
+  const int h = grp * 4 + (lane >> 4);
+  const bool active = h < heads;
+  const int d0 = (lane & 15) * 8;
+  T* p = x + row * ldx + col0 + blk * col_stride + h * 128 + d0;
+  float v[8] = {};
+  if (active) load8(p, v);
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ss += v[e] * v[e];
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if (!active) return;
+  const float r = 1.0f / sqrtf(ss / 128.0f + eps);
+  float wv[8];
+  load8(w + blk * w_stride + h * 128 + d0, wv);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = Elt<T>::rnd((v[e] * r) * wv[e]);
+  if (h < rope_heads) {
+    const int pos = pos0 + pos_mult * (row % seq_len);
+    const float* cs = rope + ((int64_t)pos * 64 + d0 / 2) * 2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float c = cs[2 * e], s = cs[2 * e + 1];
+      const float a = v[2 * e], b = v[2 * e + 1];
+      v[2 * e] = (a * c) - (b * s);
+      v[2 * e + 1] = (a * s) + (b * c);
+    }
+  }
+  store8(p, v);
+}
+
+template <typename T>
+__global__ void temb_kernel(const float* __restrict__ t, const float* __restrict__ freqs, T* __restrict__ out,
+                            int S, int half) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S * half) return;
+  const int s = i / half, k = i % half;
+  const float a = t[s] * freqs[k];
+  Elt<T>::st(out + (int64_t)s * 2 * half + k, cosf(a));
+  Elt<T>::st(out + (int64_t)s * 2 * half + half + k, sinf(a));
+}
+
+template <typename T>
+__global__ void silu_kernel(const T* __restrict__ x, int64_t ldx, T* __restrict__ y, int64_t ldy, int rows,
+                            int cols) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)rows * cols) return;
+  const int r = i / cols, c = i % cols;
+  Elt<T>::st(y + r * ldy + c, silu_f(Elt<T>::ld(x + r * ldx + c)));
+}
+
+// raw [n_ada][S][3][D] -> table [S][n_ada][3][D]
+template <typename T>
+__global__ void adaln_finish_kernel(const T* __restrict__ raw, T* __restrict__ tab, int n_ada, int S, int D) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)n_ada * S * 3 * D;
+  if (i >= total) return;
+  const int d = i % D;
+  const int c = (i / D) % 3;
+  const int s = (i / ((int64_t)3 * D)) % S;
+  const int a = i / ((int64_t)3 * D * S);
+  float v = Elt<T>::ld(raw + i);
+  if (c == 1) v = v + 1.0f;
+  if (c == 2) v = tanhf(v);
+  Elt<T>::st(tab + (((int64_t)s * n_ada + a) * 3 + c) * D + d, v);
+}
+
+template <typename T>
+__global__ void latent_in_kernel(const float* __restrict__ x, T* __restrict__ out, int rows, int C, int ldo,
+                                 int copies) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)copies * rows * ldo) return;
+  const int c = i % ldo;
+  const int64_t r = i / ldo;
+  const int src = r % rows;
+  Elt<T>::st(out + i, c < C ? x[(int64_t)src * C + c] : 0.0f);
+}
+
+// CFG combine + optional rescale + Euler: inference.py:526-530,431-443,558 (un-contracted).
+__global__ void euler_kernel(float* __restrict__ x, const float* __restrict__ v, int64_t n, EchoStepArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float vp;
+  if (a.has_cfg) {
+    const float vc = v[i], vt = v[i + n], vs = v[i + 2 * n];
+    vp = (vc + a.cfg_text * (vc - vt)) + a.cfg_speaker * (vc - vs);
+  } else {
+    vp = v[i];
+  }
+  const float xi = x[i];
+  if (a.rescale) vp = a.inv_omt * ((a.ratio * ((a.omt * vp) + xi)) - xi);
+  x[i] = xi + vp * a.dt;
+}
+
+template <typename T>
+__global__ void embed_kernel(const int32_t* __restrict__ ids, const T* __restrict__ table, T* __restrict__ out,
+                             int n, int dim) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= (int64_t)n * dim) return;
+  const int r = i / dim, c = i % dim;
+  float v[8];
+  load8(table + (int64_t)ids[r] * dim + c, v);
+  store8(out + i, v);
+}
+
+template <typename T>
+__global__ void scale_rows_kernel(T* __restrict__ x, int64_t ldx, int rows, int cols, float s) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= (int64_t)rows * cols) return;
+  const int r = i / cols, c = i % cols;
+  T* p = x + r * ldx + c;
+  float v[8];
+  load8(p, v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = v[e] * s;
+  store8(p, v);
+}
+
+template <typename T>
+__global__ void cast_kernel(const float* __restrict__ x, T* __restrict__ y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) Elt<T>::st(y + i, x[i]);
+}
+
+inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+}  // namespace
+
+#define DISPATCH(dtype, ...)                                   \
+  do {                                                         \
+    if ((dtype) == ECHO_BF16) { using T = bf16_t; __VA_ARGS__; } \
+    else if ((dtype) == ECHO_F32) { using T = float; __VA_ARGS__; } \
+    else return ECHO_EDTYPE;                                   \
+  } while (0)
+
+extern "C" {
+
+int echo_rmsnorm(int32_t dtype, const void* x, int64_t ldx, const void* w, void* y, int64_t ldy, int32_t rows,
+                 int32_t dim, float eps, void* stream) {
+  if (!x || !w || !y || rows <= 0 || dim <= 0 || dim % 8 || dim > 8 * NB * 4) return ECHO_ESHAPE;
+  if (rows == 0) return 0;
+  DISPATCH(dtype, hipLaunchKernelGGL(rmsnorm_kernel<T>, dim3(rows), dim3(NB), 0, (hipStream_t)stream,
+                                     (const T*)x, ldx, (const T*)w, (T*)y, ldy, dim, eps));
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+int echo_adaln_modulate(int32_t dtype, const void* x, void* y, int32_t rows, int32_t dim, const void* shift,
+                        const void* scale1, int32_t rows_per_vec, int64_t vec_stride, float eps, void* stream) {
+  if (!x || !y || !shift || !scale1 || rows <= 0 || dim % 8 || dim > 8 * NB * 4) return ECHO_ESHAPE;
+  if (rows_per_vec <= 0) rows_per_vec = rows;
+  DISPATCH(dtype, hipLaunchKernelGGL(adaln_kernel<T>, dim3(rows), dim3(NB), 0, (hipStream_t)stream, (const T*)x,
+                                     (T*)y, dim, (const T*)shift, (const T*)scale1, rows_per_vec, vec_stride,
+                                     eps));
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+int echo_head_norm_rope(int32_t dtype, void* x, int64_t ldx, int32_t rows, int32_t heads, int32_t nblk,
+                        int64_t col0, int64_t col_stride, const void* w, int64_t w_stride, const float* rope,
+                        int32_t rope_heads, int32_t seq_len, int32_t pos0, int32_t pos_mult, float eps,
+                        void* stream) {
+  if (!x || !w || rows <= 0 || heads <= 0 || nblk <= 0 || seq_len <= 0) return ECHO_ESHAPE;
+  if (rope_heads > 0 && !rope) return ECHO_EINVAL;
+  const int64_t tasks = (int64_t)rows * nblk * ((heads + 3) / 4);
+  DISPATCH(dtype, hipLaunchKernelGGL(head_norm_rope_kernel<T>, dim3(blocks(tasks, 4)), dim3(NB), 0,
+                                     (hipStream_t)stream, (T*)x, ldx, rows, heads, nblk, col0, col_stride,
+                                     (const T*)w, w_stride, rope, rope_heads, seq_len, pos0, pos_mult, eps));
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+int echo_timestep_embedding(int32_t dtype, const float* t, const float* freqs, void* out, int32_t S,
+                            int32_t half, void* stream) {
+  if (!t || !freqs || !out || S <= 0 || half <= 0) return ECHO_ESHAPE;
+  DISPATCH(dtype, hipLaunchKernelGGL(temb_kernel<T>, dim3(blocks((int64_t)S * half, 256)), dim3(256), 0,
+                                     (hipStream_t)stream, t, freqs, (T*)out, S, half));
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+int echo_silu(int32_t dtype, const void* x, int64_t ldx, void* y, int64_t ldy, int32_t rows, int32_t cols,
+              void* stream) {
+  if (!x || !y || rows <= 0 || cols <= 0) return ECHO_ESHAPE;
+  DISPATCH(dtype, hipLaunchKernelGGL(silu_kernel<T>, dim3(blocks((int64_t)rows * cols, 256)), dim3(256), 0,
+                                     (hipStream_t)stream, (const T*)x, ldx, (T*)y, ldy, rows, cols));
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+int echo_adaln_finish(int32_t dtype, const void* raw, void* table, int32_t n_ada, int32_t S, int32_t D,
+                      void* stream) {
+  if (!raw || !table || n_ada <= 0 || S <= 0 || D <= 0) return ECHO_ESHAPE;
+  const int64_t n = (int64_t)n_ada * S * 3 * D;
+  DISPATCH(dtype, hipLaunchKernelGGL(adaln_finish_kernel<T>, dim3(blocks(n, 256)), dim3(256), 0,
+                                     (hipStream_t)stream, (const T*)raw, (T*)table, n_ada, S, D));
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+int echo_latent_to_input(int32_t dtype, const float* x, void* out, int32_t rows, int32_t C, int32_t ld_out,
+                         int32_t copies, void* stream) {
+  if (!x || !out || rows <= 0 || C <= 0 || ld_out < C || copies <= 0) return ECHO_ESHAPE;
+  const int64_t n = (int64_t)copies * rows * ld_out;
+  DISPATCH(dtype, hipLaunchKernelGGL(latent_in_kernel<T>, dim3(blocks(n, 256)), dim3(256), 0,
+                                     (hipStream_t)stream, x, (T*)out, rows, C, ld_out, copies));
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+int echo_euler_step(float* x, const float* v, int64_t n, const EchoStepArgs* a, void* stream) {
+  if (!x || !v || !a || n <= 0) return ECHO_ESHAPE;
+  hipLaunchKernelGGL(euler_kernel, dim3(blocks(n, 256)), dim3(256), 0, (hipStream_t)stream, x, v, n, *a);
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+int echo_embed(int32_t dtype, const int32_t* ids, const void* table, void* out, int32_t n, int32_t dim,
+               void* stream) {
+  if (!ids || !table || !out || n <= 0 || dim % 8) return ECHO_ESHAPE;
+  DISPATCH(dtype, hipLaunchKernelGGL(embed_kernel<T>, dim3(blocks((int64_t)n * dim / 8, 256)), dim3(256), 0,
+                                     (hipStream_t)stream, ids, (const T*)table, (T*)out, n, dim));
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+int echo_scale_rows(int32_t dtype, void* x, int64_t ldx, int32_t rows, int32_t cols, float scale,
+                    void* stream) {
+  if (!x || rows <= 0 || cols <= 0 || cols % 8) return ECHO_ESHAPE;
+  DISPATCH(dtype, hipLaunchKernelGGL(scale_rows_kernel<T>, dim3(blocks((int64_t)rows * cols / 8, 256)),
+                                     dim3(256), 0, (hipStream_t)stream, (T*)x, ldx, rows, cols, scale));
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+int echo_cast_from_f32(int32_t dtype, const float* x, void* y, int64_t n, void* stream) {
+  if (!x || !y || n <= 0) return ECHO_ESHAPE;
+  DISPATCH(dtype, hipLaunchKernelGGL(cast_kernel<T>, dim3(blocks(n, 256)), dim3(256), 0, (hipStream_t)stream, x,
+                                     (T*)y, n));
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+const char* echo_version(void) { return "echo_hip gfx950 r1 " __DATE__ " " __TIME__; }
+
+}  // extern "C"

@@ -1,0 +1,346 @@
+// gemm.hip — C[M,N] = A[M,K] . W[N,K]^T with the fused epilogues of echo_hip.h.
+//
+// Replaces every nn.Linear on the sampling path (reference model.py:56-62,118-122,
+// 177-197,303-305,443,532-540,557) together with the elementwise tails the
+// reference runs right after them (SwiGLU, gated residual, bias, SiLU, /6, .float()).
+//
+// bf16 kernel (gfx950, MFMA v_mfma_f32_16x16x32_bf16):
+//   * tile BM x BN x 64, WM x WN waves, each wave TM x TN of 16x16 fragments;
+//   * both operands are K-contiguous rows; a K-step stages A and W tiles into LDS
+//     with global_load_lds_dwordx4 (one 1 KiB wave-instruction = 8 rows of 128 B),
+//     double-buffered, the chunk swizzle `chunk ^ ((row>>1)&7)` applied on the
+//     SOURCE address so the lane-linear LDS image is conflict-free for the
+//     16-lane ds_read_b128 groups of the fragment reads;
+//   * operands are swapped (W fragment = MFMA A, X fragment = MFMA B) so each lane
+//     ends with 4 consecutive output columns of one row;
+//   * epilogue: bias/round/act in registers, then a per-wave XOR-swizzled LDS tile,
+//     read back as 16-B row chunks for coalesced stores and the row-wise tails
+//     (residual read, gate) — one HBM pass for the whole fused tail;
+//   * block -> tile map: bijective XCD remap then group-M ordering (L2 reuse of W).
+// fp32 kernel: plain LDS-tiled FMA GEMM for the fp32 parity mode (same epilogues).
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 64;
+
+struct Epi {
+  const void* bias; int64_t stride_bias;
+  const void* aux; int64_t ld_aux, stride_aux;
+  const void* gate; int64_t stride_gate;
+  int epi, act; float out_div;
+};
+
+__device__ __forceinline__ float epi_pointwise(float v, const Epi& ep) {
+  v = rbf(v);
+  if (ep.act == ECHO_ACT_SILU) v = rbf(silu_f(v));
+  if (ep.out_div != 0.0f) v = rbf(v / ep.out_div);
+  return v;
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN)
+gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
+                 const bf16_t* __restrict__ W, int64_t ldw, int64_t sW,
+                 void* __restrict__ Cv, int64_t ldc, int64_t sC,
+                 int M, int N, int K, int tiles_m, int tiles_n, Epi ep) {
+  constexpr int NW = WM * WN;
+  constexpr int NT = 64 * NW;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int STAGE = (BM + BN) * BK;  // elements per buffer
+  static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "staging split");
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int z = blockIdx.y;
+  A += z * sA;
+  W += z * sW;
+
+  // ---- block -> tile: bijective XCD remap, then group-M ordering
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  constexpr int GM = 8;
+  const int grp = wg / (GM * tiles_n);
+  const int fm = grp * GM;
+  const int gm = min(tiles_m - fm, GM);
+  const int rem = wg - grp * GM * tiles_n;
+  const int tm = fm + rem % gm, tn = rem / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int kt, int buf) {
+    bf16_t* As = lds + buf * STAGE;
+    bf16_t* Bs = As + BM * BK;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < BM * 8 / NT; ++i) {
+      const int rb = (i * NW + wid) * 8;
+      const int row = rb + (lane >> 3);
+      const int gc = (lane & 7) ^ ((row >> 1) & 7);
+      const int grow = min(m0 + row, M - 1);
+      const bf16_t* src = A + (int64_t)grow * lda + k0 + gc * 8;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(As + rb * BK), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BN * 8 / NT; ++i) {
+      const int rb = (i * NW + wid) * 8;
+      const int row = rb + (lane >> 3);
+      const int gc = (lane & 7) ^ ((row >> 1) & 7);
+      const int grow = min(n0 + row, N - 1);
+      const bf16_t* src = W + (int64_t)grow * ldw + k0 + gc * 8;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(Bs + rb * BK), 16, 0, 0);
+    }
+  };
+
+  const int nk = K / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int frow = lane & 15;
+  const int fsw = frow >> 1;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    const bf16_t* As = lds + cur * STAGE;
+    const bf16_t* Bs = As + BM * BK;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ph = ((4 * s + (lane >> 4)) ^ fsw) * 8;
+      bf16x8 xf[FM], wf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) xf[i] = *(const bf16x8*)(As + (wm * TM + i * 16 + frow) * BK + ph);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) wf[j] = *(const bf16x8*)(Bs + (wn * TN + j * 16 + frow) * BK + ph);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue, stage 1: registers -> per-wave swizzled LDS tile (bf16-rounded)
+  const bool swiglu = ep.epi == ECHO_EPI_SWIGLU;
+  const int TNo = swiglu ? TN / 2 : TN;  // staged columns per wave row
+  const int CH = TNo / 8;                // 16-B chunks per staged row
+  bf16_t* stg = lds + wid * (TM * TN);
+  const bf16_t* biasp = ep.bias ? (const bf16_t*)ep.bias + z * ep.stride_bias : nullptr;
+  const int cq = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int ml = i * 16 + (lane & 15);
+    if (swiglu) {
+#pragma unroll
+      for (int jj = 0; jj < FN / 2; ++jj) {
+        float u[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float a = rbf(acc[i][2 * jj][r]), b = rbf(acc[i][2 * jj + 1][r]);
+          u[r] = rbf(rbf(silu_f(a)) * b);
+        }
+        const int c0 = jj * 16 + cq;
+        const int ph = ((c0 >> 3) ^ (ml & (CH - 1))) * 8 + (c0 & 7);
+        *(uint2*)(stg + ml * TNo + ph) = make_uint2(pack2bf(u[0], u[1]), pack2bf(u[2], u[3]));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        float v[4];
+        const int nl = j * 16 + cq;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = acc[i][j][r];
+          if (biasp) x += bf2f(biasp[min(n0 + wn * TN + nl + r, N - 1)]);
+          v[r] = epi_pointwise(x, ep);
+        }
+        const int ph = ((nl >> 3) ^ (ml & (CH - 1))) * 8 + (nl & 7);
+        *(uint2*)(stg + ml * TNo + ph) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+  // ---- epilogue, stage 2: row chunks -> fused row-wise tail -> 16-B stores
+  const int Nout = swiglu ? N / 2 : N;
+  const int nbase = (swiglu ? n0 / 2 : n0) + wn * TNo;
+  const int RPI = 64 / CH;
+  const int c = lane % CH;
+  for (int it = 0; it < TM / RPI; ++it) {
+    const int row = it * RPI + lane / CH;
+    const int m = m0 + wm * TM + row;
+    const int n = nbase + c * 8;
+    float v[8];
+    load8(stg + row * TNo + ((c ^ (row & (CH - 1))) * 8), v);
+    if (m >= M || n >= Nout) continue;
+    if (ep.epi == ECHO_EPI_RESID) {
+      float x[8];
+      load8((const bf16_t*)ep.aux + z * ep.stride_aux + (int64_t)m * ep.ld_aux + n, x);
+      if (ep.gate) {
+        float g[8];
+        load8((const bf16_t*)ep.gate + z * ep.stride_gate + n, g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = rbf(g[e] * v[e]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = rbf(x[e] + v[e]);
+    }
+    if (ep.epi == ECHO_EPI_F32OUT)
+      store8((float*)Cv + z * sC + (int64_t)m * ldc + n, v);
+    else
+      store8((bf16_t*)Cv + z * sC + (int64_t)m * ldc + n, v);
+  }
+}
+
+// ----------------------------------------------------------------------------- fp32 (parity mode)
+constexpr int FT = 64, FK = 16;
+
+__global__ void __launch_bounds__(256)
+gemm_f32_kernel(const float* __restrict__ A, int64_t lda, int64_t sA,
+                const float* __restrict__ W, int64_t ldw, int64_t sW,
+                void* __restrict__ Cv, int64_t ldc, int64_t sC, int M, int N, int K, Epi ep) {
+  __shared__ float As[FK][FT + 1], Ws[FK][FT + 1];
+  __shared__ float Ct[FT][FT + 1];
+  const int z = blockIdx.z;
+  A += z * sA;
+  W += z * sW;
+  const int m0 = blockIdx.y * FT, n0 = blockIdx.x * FT;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < K; k0 += FK) {
+    for (int e = threadIdx.x; e < FT * FK; e += 256) {
+      const int r = e / FK, kk = e % FK;
+      As[kk][r] = A[(int64_t)min(m0 + r, M - 1) * lda + k0 + kk];
+      Ws[kk][r] = W[(int64_t)min(n0 + r, N - 1) * ldw + k0 + kk];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < FK; ++kk) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { a[i] = As[kk][ty + 16 * i]; b[i] = Ws[kk][tx + 16 * i]; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+  const float* bias = ep.bias ? (const float*)ep.bias + z * ep.stride_bias : nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = acc[i][j];
+      const int n = n0 + tx + 16 * j;
+      if (bias && ep.epi != ECHO_EPI_SWIGLU) v += bias[min(n, N - 1)];
+      if (ep.act == ECHO_ACT_SILU) v = silu_f(v);
+      if (ep.out_div != 0.0f) v = v / ep.out_div;
+      Ct[ty + 16 * i][tx + 16 * j] = v;
+    }
+  __syncthreads();
+  if (ep.epi == ECHO_EPI_SWIGLU) {
+    for (int e = threadIdx.x; e < FT * FT / 2; e += 256) {
+      const int r = e / (FT / 2), o = e % (FT / 2);
+      const int ca = (o / 16) * 32 + (o % 16);
+      const int m = m0 + r, n = n0 / 2 + o;
+      if (m < M && n < N / 2) ((float*)Cv)[z * sC + (int64_t)m * ldc + n] = silu_f(Ct[r][ca]) * Ct[r][ca + 16];
+    }
+    return;
+  }
+  for (int e = threadIdx.x; e < FT * FT; e += 256) {
+    const int r = e / FT, cc = e % FT;
+    const int m = m0 + r, n = n0 + cc;
+    if (m >= M || n >= N) continue;
+    float v = Ct[r][cc];
+    if (ep.epi == ECHO_EPI_RESID) {
+      if (ep.gate) v = ((const float*)ep.gate)[z * ep.stride_gate + n] * v;
+      v = ((const float*)ep.aux)[z * ep.stride_aux + (int64_t)m * ep.ld_aux + n] + v;
+    }
+    ((float*)Cv)[z * sC + (int64_t)m * ldc + n] = v;
+  }
+}
+
+struct TileCfg { int bm, bn, occ; float eff; };
+constexpr TileCfg kTiles[] = {
+    {256, 256, 1, 1.00f},  // 1: 8 waves, 128x64 per wave
+    {256, 128, 1, 0.92f},  // 2: 8 waves, 64x64 per wave
+    {128, 128, 2, 0.80f},  // 3: 4 waves, 64x64 per wave
+    {128, 64, 3, 0.62f},   // 4: 4 waves, 64x32 per wave
+    {64, 64, 4, 0.40f},    // 5: 4 waves, 32x32 per wave
+};
+
+int pick_tile(int M, int N, int K, int batch) {
+  (void)K;
+  int best = 1;
+  double best_t = 1e300;
+  for (int c = 0; c < 5; ++c) {
+    const TileCfg& t = kTiles[c];
+    const double tiles = (double)((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn) * batch;
+    const double rounds = ceil(tiles / (256.0 * t.occ));
+    const double est = rounds * t.occ * (double)t.bm * t.bn / t.eff;
+    if (est < best_t * 0.999) { best_t = est; best = c + 1; }
+  }
+  return best;
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_bf16(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
+  const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;
+  dim3 grid(tm * tn, a->batch);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN>), grid, dim3(64 * WM * WN), 0, s,
+                     (const bf16_t*)a->A, a->lda, a->stride_a, (const bf16_t*)a->W, a->ldw, a->stride_w,
+                     a->C, a->ldc, a->stride_c, a->M, a->N, a->K, tm, tn, ep);
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
+  if (!a || !a->A || !a->W || !a->C) return ECHO_EINVAL;
+  if (a->M <= 0 || a->N <= 0 || a->K <= 0 || a->batch <= 0) return ECHO_ESHAPE;
+  if (a->K % 64 || a->N % 16 || a->lda % 8 || a->ldw % 8 || a->ldc % 8) return ECHO_EALIGN;
+  if (a->epilogue == ECHO_EPI_RESID && !a->aux) return ECHO_EINVAL;
+  if (a->epilogue == ECHO_EPI_SWIGLU && (a->N % 32 || a->bias)) return ECHO_EINVAL;
+  if (a->epilogue < 0 || a->epilogue > 3) return ECHO_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  Epi ep{a->bias, a->stride_bias, a->aux, a->ld_aux, a->stride_aux, a->gate, a->stride_gate,
+         a->epilogue, a->act, a->out_div};
+  if (a->dtype == ECHO_F32) {
+    dim3 grid((a->N + FT - 1) / FT, (a->M + FT - 1) / FT, a->batch);
+    hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, s, (const float*)a->A, a->lda, a->stride_a,
+                       (const float*)a->W, a->ldw, a->stride_w, a->C, a->ldc, a->stride_c, a->M, a->N,
+                       a->K, ep);
+    ECHO_LAUNCH_CHECK();
+    return 0;
+  }
+  if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
+  if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C) & 15) return ECHO_EALIGN;
+  int t = a->tile > 0 ? a->tile : pick_tile(a->M, a->N, a->K, a->batch);
+  switch (t) {
+    case 1: return launch_bf16<256, 256, 2, 4>(a, ep, s);
+    case 2: return launch_bf16<256, 128, 4, 2>(a, ep, s);
+    case 3: return launch_bf16<128, 128, 2, 2>(a, ep, s);
+    case 4: return launch_bf16<128, 64, 2, 2>(a, ep, s);
+    case 5: return launch_bf16<64, 64, 2, 2>(a, ep, s);
+    default: return ECHO_EINVAL;
+  }
+}

@@ -1,0 +1,177 @@
+"""Static-buffer Euler-CFG engine: one plan per shape signature, the step loop
+captured as a hipGraph (torch.cuda.CUDAGraph over the HIP stream).
+
+Everything data-dependent in the reference loop (inference.py:508-558) is
+resolved on the host BEFORE the loop, in fp32 CPU tensors exactly as the
+reference computes it (so no device->host sync remains inside the loop):
+  * t_i = linspace(1, 0, S+1)[i] * 0.999                      (inference.py:477)
+  * has_cfg_i = (t_i >= cfg_min_t) * (t_i <= cfg_max_t)        (inference.py:511)
+  * dt_i = t_{i+1} - t_i, rescale coefficients                (inference.py:431-443,558)
+  * the step at which the speaker-KV scale is undone           (inference.py:546-556)
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import torch
+
+from . import _lib as L
+from . import ops
+from .model import EchoDiTHip, KVStore, Workspace
+
+INIT_SCALE = 0.999  # inference.py:470
+
+
+@dataclass(frozen=True)
+class Schedule:
+    steps: int
+    t: Tuple[float, ...]            # t_0 .. t_S (fp32 values)
+    has_cfg: Tuple[bool, ...]
+    args: Tuple[Tuple, ...]         # per-step EchoStepArgs fields
+    unscale_step: Optional[int]     # step after which speaker KV is divided by its scale
+
+
+def make_schedule(num_steps: int, cfg_scale_text: float, cfg_scale_speaker: float, cfg_min_t: float,
+                  cfg_max_t: float, rescale_k: Optional[float], rescale_sigma: Optional[float],
+                  speaker_kv_scale: Optional[float], speaker_kv_min_t: Optional[float]) -> Schedule:
+    ts = torch.linspace(1.0, 0.0, num_steps + 1) * INIT_SCALE
+    has_cfg, args = [], []
+    unscale = None
+    for i in range(num_steps):
+        t, tn = ts[i], ts[i + 1]
+        cfg = bool(((t >= cfg_min_t) * (t <= cfg_max_t)).item())
+        dt = float(tn - t)
+        resc, omt, ratio, inv = 0, 0.0, 0.0, 0.0
+        if rescale_k is not None and rescale_sigma is not None and bool(t < 1):
+            snr = (1 - t) ** 2 / (t ** 2)
+            r = (snr * rescale_sigma ** 2 + 1) / (snr * rescale_sigma ** 2 / rescale_k + 1)
+            resc, omt, ratio, inv = 1, float(1 - t), float(r), float(1 / (1 - t))
+        has_cfg.append(cfg)
+        args.append((int(cfg), float(cfg_scale_text), float(cfg_scale_speaker), resc, omt, ratio, inv, dt))
+        if speaker_kv_scale is not None and bool(tn < speaker_kv_min_t) and bool(t >= speaker_kv_min_t):
+            unscale = i  # the reference's condition can only hold once on a decreasing schedule
+    return Schedule(num_steps, tuple(float(v) for v in ts), tuple(has_cfg), tuple(args), unscale)
+
+
+def step_args(fields: Tuple) -> L.StepArgs:
+    a = L.StepArgs()
+    (a.has_cfg, a.cfg_text, a.cfg_speaker, a.rescale, a.omt, a.ratio, a.inv_omt, a.dt) = fields
+    return a
+
+
+def round_up(v: int, m: int) -> int:
+    return (v + m - 1) // m * m
+
+
+def kv_scale_cols(model: EchoDiTHip, max_layers: Optional[int]) -> int:
+    """Leading columns of a [tokens, L*2*D] KV row covered by the first `max_layers` layers."""
+    nl = model.cfg.num_layers if max_layers is None else min(max_layers, model.cfg.num_layers)
+    return nl * 2 * model.cfg.model_size
+
+
+class CFGPlan:
+    """Buffers + (optional) captured graph for one (B, N, text cap, speaker cap, schedule)."""
+
+    def __init__(self, model: EchoDiTHip, B: int, N: int, Tc: int, Pc: int, sched: Schedule,
+                 kv_scale: Optional[float], kv_max_layers: Optional[int]):
+        self.m, self.B, self.N, self.Tc, self.Pc, self.sched = model, B, N, Tc, Pc, sched
+        cfg = model.cfg
+        dev, dt = model.device, model.dtype
+        D, H, nl = cfg.model_size, cfg.num_heads, cfg.num_layers
+        any_cfg = any(sched.has_cfg)
+        self.ws = Workspace((3 if any_cfg else 1) * B * N, cfg, dev, dt)
+        self.x = torch.empty((B, N, cfg.latent_size), device=dev, dtype=torch.float32)
+        self.kv_text = torch.empty((B, Tc, nl, 2, H, 128), device=dev, dtype=dt)
+        self.kv_spk = torch.empty((B, Pc, nl, 2, H, 128), device=dev, dtype=dt) if Pc > 0 else None
+        self.table = torch.empty((sched.steps, 2 * nl, 3, D), device=dev, dtype=dt)
+        self.lens = torch.zeros((4, 3 * B), device=dev, dtype=torch.int32)  # text3, spk3, text1, spk1
+        self.kv_scale, self.kv_cols = kv_scale, kv_scale_cols(model, kv_max_layers)
+        self.args = [step_args(a) for a in sched.args]
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.runs = 0
+
+    # -- per call
+    def setup(self, ids, text_mask, speaker_latent, speaker_mask, noise, truncation_factor):
+        m, B = self.m, self.B
+        kt = m.text_kv(ids, text_mask, trim=True, cap=self.Tc, out=self.kv_text)
+        if kt.capacity != self.Tc:
+            raise RuntimeError("text capacity mismatch")
+        if self.Pc > 0:
+            ks = m.speaker_kv(speaker_latent, speaker_mask, trim=True, cap=self.Pc, out=self.kv_spk)
+            s_lens = ks.lens
+            if self.kv_scale is not None:
+                self._scale_speaker(self.kv_scale)
+        else:
+            s_lens = [0] * B
+        t_lens = kt.lens
+        host = torch.zeros((4, 3 * B), dtype=torch.int32)
+        host[0] = torch.tensor(t_lens + [0] * B + t_lens, dtype=torch.int32)     # [cond | uncond-text | cond]
+        host[1] = torch.tensor(s_lens + s_lens + [0] * B, dtype=torch.int32)     # [cond | cond | uncond-spk]
+        host[2, :B] = torch.tensor(t_lens, dtype=torch.int32)
+        host[3, :B] = torch.tensor(s_lens, dtype=torch.int32)
+        self.lens.copy_(host.to(self.lens.device, non_blocking=False))
+        self.table.copy_(m.adaln_table(self.sched.t[:-1]))
+        self.x.copy_(noise)
+        if truncation_factor is not None:
+            ops.scale_rows(self.x.view(-1, self.x.shape[-1]), self.x.shape[-1], float(truncation_factor))
+
+    def _scale_speaker(self, s: float):
+        if self.kv_spk is not None:
+            ops.scale_rows(self.kv_spk.view(self.B * self.Pc, -1), self.kv_cols, float(s))
+
+    def _segs(self, cfg_step: bool):
+        B = self.B
+        i0 = 0 if cfg_step else 2
+
+        def per_layer(i):
+            t = ops.Segment(self.kv_text[:, :, i, 0], self.kv_text[:, :, i, 1], lens=self.lens[i0], batch_mod=B)
+            s = None
+            if self.kv_spk is not None:
+                s = ops.Segment(self.kv_spk[:, :, i, 0], self.kv_spk[:, :, i, 1], lens=self.lens[i0 + 1],
+                                batch_mod=B)
+            return [None, t, s]
+        return per_layer
+
+    # -- the capturable step loop (inference.py:508-558)
+    def loop(self):
+        m, B, N = self.m, self.B, self.N
+        seg_cfg, seg_plain = self._segs(True), self._segs(False)
+        for i in range(self.sched.steps):
+            cfg_step = self.sched.has_cfg[i]
+            copies = 3 if cfg_step else 1
+            R = copies * B
+            ws = self.ws.view(R * N)
+            ops.latent_to_input(self.x, ws.xin, copies)
+            m.decoder(ws, R, N, self.table[i], seg_cfg if cfg_step else seg_plain, 0)
+            ops.euler_step(self.x, ws.v, self.args[i])
+            if self.sched.unscale_step == i and self.kv_scale is not None:
+                self._scale_speaker(1.0 / self.kv_scale)
+
+    def run(self, use_graph: bool) -> torch.Tensor:
+        if use_graph and self.runs > 0:
+            if self.graph is None:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self.loop()
+                self.graph = g
+            self.graph.replay()
+        else:
+            self.loop()
+        self.runs += 1
+        return self.x
+
+
+def plan_key(B, N, Tc, Pc, sched: Schedule, kv_scale, kv_max_layers):
+    return (B, N, Tc, Pc, sched, kv_scale, kv_max_layers)
+
+
+def get_plan(model: EchoDiTHip, B: int, N: int, Tc: int, Pc: int, sched: Schedule,
+             kv_scale: Optional[float], kv_max_layers: Optional[int]) -> CFGPlan:
+    cache = model.__dict__.setdefault("_plans", {})
+    key = plan_key(B, N, Tc, Pc, sched, kv_scale, kv_max_layers)
+    if key not in cache:
+        if len(cache) >= 4:
+            cache.pop(next(iter(cache)))
+        cache[key] = CFGPlan(model, B, N, Tc, Pc, sched, kv_scale, kv_max_layers)
+    return cache[key]

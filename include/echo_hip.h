@@ -1,0 +1,162 @@
+/*
+ * echo_hip.h — C ABI of the MI355X-native Echo-TTS sampling path.
+ *
+ * The reference path is pure Python/PyTorch: its "FFI" is the
+ * set of torch ops the DiT forward issues. Each entry point below replaces one
+ * group of those ops (file:line cited per function) and is bound from Python
+ * with ctypes (echo-tts_amd/_lib.py; the binding a maintainer would add to the
+ * reference is shown in INTEGRATION.md).
+ *
+ * Conventions (all functions):
+ *   - plain device pointers + sizes; no torch types;
+ *   - `dtype` selects the element type of activations/weights:
+ *       ECHO_BF16 (0) = bfloat16 storage, ECHO_F32 (1) = float32;
+ *   - `stream` is a hipStream_t (NULL = default stream); nothing here
+ *     synchronises the host, so every call is capturable in a hipGraph;
+ *   - return 0 on success, a negative ECHO_E* code on invalid arguments
+ *     (checked on the host before launch), or a positive hipError_t.
+ *   - lengths/masks are prefix lengths: a key mask of the reference
+ *     (model.py:246-261) must be a prefix to be expressible (host checks it).
+ */
+#ifndef ECHO_HIP_H
+#define ECHO_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ECHO_BF16 = 0, ECHO_F32 = 1 };
+enum { ECHO_OK = 0, ECHO_EINVAL = -1, ECHO_EDTYPE = -2, ECHO_ESHAPE = -3, ECHO_EALIGN = -4 };
+
+/* GEMM epilogues (applied in this order; see echo-tts_amd/csrc/gemm.hip):
+ *   v = acc (+ bias[n]);  v = round(v)                       F.linear (model.py:56-62,303-305,...)
+ *   act == ECHO_ACT_SILU: v = round(silu(v))                 nn.SiLU in cond_module (model.py:532-538)
+ *   out_div != 0:         v = round(v / out_div)             SpeakerEncoder `x / 6.` (model.py:462)
+ *   ECHO_EPI_SWIGLU: W rows interleaved in blocks of 16 (w1,w3,w1,w3,...);
+ *                    out[m][n] = round(round(silu(a)) * b)   MLP.forward (model.py:307-308)
+ *   ECHO_EPI_RESID:  out = round(aux[m][n] + round(gate[n] * v))   gated residual (model.py:385,388)
+ *                    (gate NULL: out = round(aux + v); aux may alias out)
+ *   ECHO_EPI_F32OUT: out (float32) = v                       out_proj(...).float() (model.py:602-604)
+ */
+enum { ECHO_EPI_STORE = 0, ECHO_EPI_SWIGLU = 1, ECHO_EPI_RESID = 2, ECHO_EPI_F32OUT = 3 };
+enum { ECHO_ACT_NONE = 0, ECHO_ACT_SILU = 1 };
+
+typedef struct {
+  int32_t dtype;
+  int32_t M, N, K;          /* C[M,N] = A[M,K] . W[N,K]^T ; K % 64 == 0, N % 16 == 0 */
+  int32_t batch;            /* grid.y batches, strides in elements */
+  const void* A; int64_t lda; int64_t stride_a;
+  const void* W; int64_t ldw; int64_t stride_w;
+  void* C; int64_t ldc; int64_t stride_c;
+  const void* bias; int64_t stride_bias;          /* [N] or NULL */
+  const void* aux; int64_t ld_aux; int64_t stride_aux;  /* RESID residual input */
+  const void* gate; int64_t stride_gate;          /* RESID per-column gate or NULL */
+  int32_t epilogue, act;
+  float out_div;
+  int32_t tile;             /* 0 = auto; else forced config id (tests/tuning) */
+} EchoGemmArgs;
+
+/* Replaces every nn.Linear of the DiT and its encoders (F.linear, model.py:56-62,
+ * 118-122,177-197,303-305,443,532-540,557) plus the fused elementwise tails above. */
+int echo_gemm(const EchoGemmArgs* args, void* stream);
+
+/* One key/value segment of the joint attention (model.py:246-253): rows of
+ * `len[row]` valid tokens (prefix), head h at element offset h*128. */
+typedef struct {
+  const void* k; const void* v;
+  int64_t ld_tok;     /* elements between consecutive tokens */
+  int64_t ld_batch;   /* elements between batch entries */
+  int32_t batch_mod;  /* batch entry used by decoder row r: r % batch_mod */
+  int32_t capacity;   /* tokens stored per batch entry (loads are clamped to it) */
+  const int32_t* len; /* [rows] valid prefix lengths (device), NULL = capacity */
+  int32_t causal;     /* key j visible to query i iff j <= i (encoder self-attention) */
+} EchoKVSegment;
+
+typedef struct {
+  int32_t dtype;
+  int32_t rows, n_q, heads, nseg;
+  const void* q; int64_t q_ld_tok, q_ld_batch;
+  const void* gate; int64_t g_ld_tok, g_ld_batch;  /* out *= sigmoid(gate) (model.py:157,264); NULL = none */
+  void* out; int64_t o_ld_tok, o_ld_batch;
+  float scale;              /* softmax scale, 1/sqrt(128) */
+  EchoKVSegment seg[4];     /* [self | latent | text | speaker] */
+} EchoAttnArgs;
+
+/* Replaces the KV concat + F.scaled_dot_product_attention + sigmoid gate of
+ * JointAttention.forward (model.py:237-264) and SelfAttention.forward (model.py:144-157). */
+int echo_attention(const EchoAttnArgs* args, void* stream);
+
+/* RMSNorm(x)*w in fp32, cast back (model.py:99-104). Row stride in elements. */
+int echo_rmsnorm(int32_t dtype, const void* x, int64_t ldx, const void* w, void* y, int64_t ldy,
+                 int32_t rows, int32_t dim, float eps, void* stream);
+
+/* LowRankAdaLN normalisation tail: y = round((x*rsqrt(mean x^2+eps))*scale1 + shift)
+ * with precomputed scale1 = round(scale+1) and shift (model.py:76-83). Row r uses the
+ * vectors at offset (r / rows_per_vec) * vec_stride (rows_per_vec <= 0: one vector). */
+int echo_adaln_modulate(int32_t dtype, const void* x, void* y, int32_t rows, int32_t dim,
+                        const void* shift, const void* scale1, int32_t rows_per_vec,
+                        int64_t vec_stride, float eps, void* stream);
+
+/* Per-head RMSNorm (+ RoPE on heads [0, rope_heads)) applied in place to `nblk`
+ * column blocks of `heads*128` elements: block b starts at column col0 + b*col_stride
+ * and uses norm weight w + b*w_stride ([heads,128]). Position of row i is
+ * pos0 + pos_mult*(i % seq_len); rope table = float2 (cos,sin) [positions][64].
+ * Covers q_norm/k_norm + _apply_rotary_half / apply_rotary_emb (model.py:138-142,
+ * 221-232,274,281,289-291). rope_heads = 0 disables RoPE. */
+int echo_head_norm_rope(int32_t dtype, void* x, int64_t ldx, int32_t rows, int32_t heads,
+                        int32_t nblk, int64_t col0, int64_t col_stride, const void* w, int64_t w_stride,
+                        const float* rope, int32_t rope_heads, int32_t seq_len, int32_t pos0,
+                        int32_t pos_mult, float eps, void* stream);
+
+/* Timestep embedding [cos|sin](float(t_s) * freqs) cast to dtype (model.py:27-43).
+ * t: [S] floats already rounded to the model dtype; freqs: [half] fp32; out [S, 2*half]. */
+int echo_timestep_embedding(int32_t dtype, const float* t, const float* freqs, void* out,
+                            int32_t S, int32_t half, void* stream);
+
+/* y = round(silu(x)) elementwise over a [rows, cols] block with strides (model.py:72-74). */
+int echo_silu(int32_t dtype, const void* x, int64_t ldx, void* y, int64_t ldy, int32_t rows,
+              int32_t cols, void* stream);
+
+/* AdaLN table finish: raw [n_ada][S][3][D] (shift, scale, gate after the low-rank
+ * refinement) -> table [S][n_ada][3][D] with (shift, round(scale+1), round(tanh(gate)))
+ * (model.py:72-81). */
+int echo_adaln_finish(int32_t dtype, const void* raw, void* table, int32_t n_ada, int32_t S,
+                      int32_t D, void* stream);
+
+/* Sampler state -> model input: out[c*B*N + i][0:C] = round(x[i][0:C]), zero-padded to
+ * ld_out columns, for c in [0, copies) (torch.cat([x,x,x]).to(dtype), inference.py:516,533). */
+int echo_latent_to_input(int32_t dtype, const float* x, void* out, int32_t rows, int32_t C,
+                         int32_t ld_out, int32_t copies, void* stream);
+
+/* Fused CFG combine + temporal score rescale + Euler update on the fp32 state
+ * (inference.py:526-530,431-443,542-543,558). v: [R][n] with R = 3 (cfg) or 1 blocks
+ * of n = B*N*80 elements. Scalars precomputed on the host in fp32 exactly as the
+ * reference computes them. */
+typedef struct {
+  int32_t has_cfg; float cfg_text, cfg_speaker;
+  int32_t rescale; float omt, ratio, inv_omt;   /* 1-t, ratio, 1/(1-t) */
+  float dt;                                     /* t_next - t */
+} EchoStepArgs;
+int echo_euler_step(float* x, const float* v, int64_t n, const EchoStepArgs* a, void* stream);
+
+/* Byte-embedding gather: out[i] = table[ids[i]] (nn.Embedding, model.py:403,420). */
+int echo_embed(int32_t dtype, const int32_t* ids, const void* table, void* out, int32_t n,
+               int32_t dim, void* stream);
+
+/* In-place x[r][0:cols] = round(x * scale) on a strided block (KV speaker scaling,
+ * Tensor.mul_ on bf16, inference.py:420-428). */
+int echo_scale_rows(int32_t dtype, void* x, int64_t ldx, int32_t rows, int32_t cols, float scale,
+                    void* stream);
+
+/* fp32 -> dtype cast of n elements (speaker_latent.to(dtype), inference.py:483). */
+int echo_cast_from_f32(int32_t dtype, const float* x, void* y, int64_t n, void* stream);
+
+/* Library identification (build stamp) — for load checks. */
+const char* echo_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ECHO_HIP_H */

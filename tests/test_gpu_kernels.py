@@ -1,0 +1,296 @@
+"""Kernel unit tests: every HIP op (called through the C ABI via ctypes) against a
+plain PyTorch reference of the same op with the reference model's rounding points.
+
+Tolerances: bf16 outputs may differ by one bf16 ulp where the fp32 accumulation
+order differs (MFMA vs fp64), so the checks are rel-L2 <= 4e-3 and
+max |diff| <= 2^-6 * max(1, |ref|); fp32 outputs rel-L2 <= 1e-5.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import echo_tts_amd  # noqa: E402
+from echo_tts_amd import _lib as L  # noqa: E402
+from echo_tts_amd import ops  # noqa: E402
+
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def close_bf16(out, ref):
+    o, r = out.float().cpu(), ref.float().cpu()
+    assert torch.isfinite(o).all()
+    assert rel(o, r) < 4e-3, rel(o, r)
+    bad = (o - r).abs() > (2 ** -6) * r.abs().clamp_min(1.0)
+    assert not bad.any(), f"{int(bad.sum())} elements off, max {float((o - r).abs().max())}"
+
+
+def rb(x):
+    return x.to(BF).float()
+
+
+def ref_linear(a, w, bias=None):
+    y = a.double().cpu() @ w.double().cpu().T
+    if bias is not None:
+        y = y + bias.double().cpu()
+    return y.float()
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("M,N,K", [(640, 2048, 2048), (200, 208, 320), (1, 80, 128), (1000, 4096, 576)])
+def test_gemm_store_bias(tile, M, N, K):
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    b = (torch.randn(N, device=DEV) * 0.1).to(BF)
+    out = ops.gemm(a, w, bias=b, tile=tile)
+    close_bf16(out, rb(ref_linear(a, w, b)))
+
+
+@pytest.mark.parametrize("tile", [1, 3, 5])
+def test_gemm_swiglu(tile):
+    M, F, K = 333, 704, 256
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w1 = (torch.randn(F, K, device=DEV) * 0.05).to(BF)
+    w3 = (torch.randn(F, K, device=DEV) * 0.05).to(BF)
+    from echo_tts_amd.model import interleave16
+    out = ops.gemm(a, interleave16(w1, w3), epilogue=L.EPI_SWIGLU, tile=tile)
+    x1, x3 = rb(ref_linear(a, w1)), rb(ref_linear(a, w3))
+    ref = rb(rb(torch.nn.functional.silu(x1)) * x3)
+    close_bf16(out, ref)
+
+
+@pytest.mark.parametrize("tile", [1, 2, 4])
+@pytest.mark.parametrize("with_gate", [True, False])
+def test_gemm_resid(tile, with_gate):
+    M, N, K = 517, 512, 1024
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.03).to(BF)
+    h = torch.randn(M, N, device=DEV).to(BF)
+    g = torch.tanh(torch.randn(N, device=DEV)).to(BF) if with_gate else None
+    ref_h = h.float().cpu().clone()
+    y = rb(ref_linear(a, w))
+    if g is not None:
+        y = rb(g.float().cpu() * y)
+    ref = rb(ref_h + y)
+    ops.gemm(a, w, out=h, epilogue=L.EPI_RESID, aux=h, gate=g, tile=tile)
+    close_bf16(h, ref)
+
+
+def test_gemm_act_div_f32out_batched():
+    a = torch.randn(40, 512, device=DEV).to(BF)
+    w = (torch.randn(256, 512, device=DEV) * 0.05).to(BF)
+    out = ops.gemm(a, w, act=L.ACT_SILU)
+    close_bf16(out, rb(torch.nn.functional.silu(rb(ref_linear(a, w)))))
+    b = (torch.randn(256, device=DEV) * 0.1).to(BF)
+    out = ops.gemm(a, w, bias=b, out_div=6.0)
+    close_bf16(out, rb(rb(ref_linear(a, w, b)) / 6.0))
+    wo = (torch.randn(80, 512, device=DEV) * 0.05).to(BF)
+    bo = (torch.randn(80, device=DEV) * 0.1).to(BF)
+    o32 = ops.gemm(a, wo, bias=bo, epilogue=L.EPI_F32OUT)
+    assert o32.dtype == torch.float32
+    close_bf16(o32, rb(ref_linear(a, wo, bo)))
+    # batched with strided A (the AdaLN-up shape) and broadcast aux
+    S, nb, r, D = 7, 6, 64, 256
+    down = torch.randn(S, nb * r, device=DEV).to(BF)
+    a3 = down.view(S, nb, r).permute(1, 0, 2)
+    wu = (torch.randn(nb, D, r, device=DEV) * 0.05).to(BF)
+    bu = (torch.randn(nb, D, device=DEV) * 0.1).to(BF)
+    cc = torch.randn(S, D, device=DEV).to(BF)
+    raw = torch.empty(nb, S, 3, D, device=DEV, dtype=BF)
+    ops.gemm(a3, wu, out=raw[:, :, 1, :], bias=bu, epilogue=L.EPI_RESID, aux=cc.unsqueeze(0).expand(nb, S, D))
+    for i in range(nb):
+        ref = rb(cc.float().cpu() + rb(ref_linear(a3[i], wu[i], bu[i])))
+        close_bf16(raw[i, :, 1], ref)
+
+
+def test_gemm_f32():
+    M, N, K = 130, 96, 192
+    a = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV) * 0.1
+    b = torch.randn(N, device=DEV)
+    out = ops.gemm(a, w, bias=b)
+    assert rel(out, ref_linear(a, w, b)) < 1e-5
+    h = torch.randn(M, N, device=DEV)
+    g = torch.randn(N, device=DEV)
+    ref = h.cpu() + g.cpu() * ref_linear(a, w)
+    ops.gemm(a, w, out=h, epilogue=L.EPI_RESID, aux=h, gate=g)
+    assert rel(h, ref) < 1e-5
+
+
+def test_gemm_rejects_bad_args():
+    a = torch.randn(16, 100, device=DEV).to(BF)
+    w = torch.randn(32, 100, device=DEV).to(BF)
+    with pytest.raises(RuntimeError, match="EALIGN"):
+        ops.gemm(a, w)
+
+
+def ref_attention(q, segs, gate, scale, dtype):
+    """fp64 softmax over the valid prefix of each segment; P rounded like the kernel is not modelled."""
+    R, nq, H, _ = q.shape
+    out = torch.empty(R, nq, H, 128, dtype=torch.float64)
+    qd = q.double().cpu()
+    for r in range(R):
+        ks, vs, masks = [], [], []
+        for s in segs:
+            b = r % (s.batch_mod or s.k.shape[0])
+            n = s.k.shape[1] if s.lens is None else int(s.lens[r])
+            ks.append(s.k[b, :n].double().cpu())
+            vs.append(s.v[b, :n].double().cpu())
+            if s.causal:
+                masks.append(torch.arange(n)[None, :] <= torch.arange(nq)[:, None])
+            else:
+                masks.append(torch.ones(nq, n, dtype=torch.bool))
+        K, V, Mk = torch.cat(ks), torch.cat(vs), torch.cat(masks, 1)
+        for h in range(H):
+            sc = qd[r, :, h] @ K[:, h].T * scale
+            sc = sc.masked_fill(~Mk, float("-inf"))
+            p = torch.softmax(sc, -1)
+            out[r, :, h] = p @ V[:, h]
+    o = out.float()
+    if dtype == BF:
+        o = rb(o)
+        if gate is not None:
+            o = rb(o * rb(torch.sigmoid(gate.float().cpu())))
+    elif gate is not None:
+        o = o * torch.sigmoid(gate.float().cpu())
+    return o
+
+
+@pytest.mark.parametrize("dtype", [BF, torch.float32])
+def test_attention_segments(dtype):
+    B, N, H = 2, 200, 4
+    R = 3 * B
+    qkvg = torch.randn(R, N, 4, H, 128, device=DEV).to(dtype)
+    kt = torch.randn(B, 96, 2, H, 128, device=DEV).to(dtype)
+    ksp = torch.randn(B, 40, 2, H, 128, device=DEV).to(dtype)
+    tl = torch.tensor([50, 71, 0, 0, 50, 71], dtype=torch.int32, device=DEV)
+    sl = torch.tensor([40, 17, 40, 17, 0, 0], dtype=torch.int32, device=DEV)
+    segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2]),
+            ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=B),
+            ops.Segment(ksp[:, :, 0], ksp[:, :, 1], lens=sl, batch_mod=B)]
+    out = torch.empty(R, N, H, 128, device=DEV, dtype=dtype)
+    ops.attention(qkvg[:, :, 0], segs, out=out, gate=qkvg[:, :, 3])
+    ref = ref_attention(qkvg[:, :, 0], segs, qkvg[:, :, 3], 128 ** -0.5, dtype)
+    if dtype == BF:
+        assert rel(out, ref) < 6e-3
+    else:
+        assert rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [BF, torch.float32])
+@pytest.mark.parametrize("L_", [160, 37])
+def test_attention_causal(dtype, L_):
+    B, H = 2, 3
+    qkv = torch.randn(B, L_, 4, H, 128, device=DEV).to(dtype)
+    segs = [ops.Segment(qkv[:, :, 1], qkv[:, :, 2], causal=True)]
+    out = torch.empty(B, L_, H, 128, device=DEV, dtype=dtype)
+    ops.attention(qkv[:, :, 0], segs, out=out, gate=None)
+    ref = ref_attention(qkv[:, :, 0], segs, None, 128 ** -0.5, dtype)
+    assert rel(out, ref) < (6e-3 if dtype == BF else 1e-5)
+
+
+def test_attention_key_padding_spike():
+    """A large score in the last valid key forces the online-softmax rescale branch."""
+    B, N, H = 1, 130, 1
+    qkv = torch.randn(B, N, 4, H, 128, device=DEV)
+    qkv[:, 100, 1] *= 20.0  # spike key 100 (in the second 64-key tile)
+    qkv = qkv.to(BF)
+    lens = torch.tensor([101], dtype=torch.int32, device=DEV)
+    segs = [ops.Segment(qkv[:, :, 1], qkv[:, :, 2], lens=lens)]
+    out = torch.empty(B, N, H, 128, device=DEV, dtype=BF)
+    ops.attention(qkv[:, :, 0], segs, out=out)
+    ref = ref_attention(qkv[:, :, 0], segs, None, 128 ** -0.5, BF)
+    assert rel(out, ref) < 6e-3
+
+
+@pytest.mark.parametrize("dtype", [BF, torch.float32])
+def test_norms(dtype):
+    x = torch.randn(37, 1280, device=DEV).to(dtype)
+    w = (1 + 0.1 * torch.randn(1280, device=DEV)).to(dtype)
+    xf = x.float().cpu()
+    r = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)
+    ref = (xf * r) * w.float().cpu()
+    out = ops.rmsnorm(x, w, 1e-5)
+    (close_bf16 if dtype == BF else lambda o, rr: rel(o, rr) < 1e-6)(out, ref.to(dtype).float())
+    sh = torch.randn(1280, device=DEV).to(dtype)
+    s1 = (1 + 0.1 * torch.randn(1280, device=DEV)).to(dtype)
+    y = torch.empty_like(x)
+    ops.adaln_modulate(x, sh, s1, 1e-5, y)
+    ref = ((xf * r) * s1.float().cpu()) + sh.float().cpu()
+    if dtype == BF:
+        close_bf16(y, rb(ref))
+    else:
+        assert rel(y, ref) < 1e-6
+
+
+@pytest.mark.parametrize("dtype", [BF, torch.float32])
+def test_head_norm_rope(dtype):
+    from oracle import echo_oracle as O
+    from echo_tts_amd.model import rope_table_cpu
+    B, N, H = 2, 33, 4
+    x = torch.randn(B * N, 4 * H * 128, device=DEV).to(dtype)
+    w = (1 + 0.1 * torch.randn(2, H, 128, device=DEV)).to(dtype)
+    rope = rope_table_cpu(128, 256).to(DEV)
+    x0 = x.clone().cpu()
+    ops.head_norm_rope(x, H, w, 1e-5, nblk=2, col0=0, col_stride=H * 128, w_stride=H * 128, rope=rope,
+                       rope_heads=H // 2, seq_len=N, pos0=5)
+    table = O.rope_table(128, 256)[5:5 + N]
+    for blk in range(2):
+        v = x0[:, blk * H * 128:(blk + 1) * H * 128].reshape(B, N, H, 128)
+        ref = O.rotate_half_heads(O.rms(v, w[blk].cpu(), 1e-5), table)
+        got = x[:, blk * H * 128:(blk + 1) * H * 128].reshape(B, N, H, 128)
+        if dtype == BF:
+            close_bf16(got, ref.float())
+        else:
+            assert rel(got, ref) < 1e-6
+    # untouched columns
+    assert torch.equal(x[:, 2 * H * 128:].cpu(), x0[:, 2 * H * 128:])
+
+
+def test_euler_step_matches_reference_expression():
+    from echo_tts_amd import engine as En
+    B, N = 2, 50
+    x = torch.randn(B, N, 80, device=DEV)
+    v = torch.randn(3, B, N, 80, device=DEV)
+    sched = En.make_schedule(10, 3.0, 5.0, 0.5, 1.0, 1.2, 3.0, None, None)
+    i = 1
+    xr = x.cpu().clone()
+    vc, vt, vs = v.cpu()
+    vp = vc + 3.0 * (vc - vt) + 5.0 * (vc - vs)
+    ts = torch.linspace(1.0, 0.0, 11) * 0.999
+    from echo_tts_amd.inference import _temporal_score_rescale
+    vp = _temporal_score_rescale(vp, xr, ts[i], 1.2, 3.0)
+    ref = xr + vp * (ts[i + 1] - ts[i])
+    ops.euler_step(x, v, En.step_args(sched.args[i]))
+    assert torch.equal(x.cpu(), ref), float((x.cpu() - ref).abs().max())
+
+
+def test_small_ops():
+    ids = torch.randint(0, 256, (3, 17), dtype=torch.int32, device=DEV)
+    tab = torch.randn(256, 128, device=DEV).to(BF)
+    out = torch.empty(3 * 17, 128, device=DEV, dtype=BF)
+    ops.embed(ids, tab, out)
+    assert torch.equal(out.cpu(), tab.cpu()[ids.cpu().long().flatten()])
+    x = torch.randn(5, 64, device=DEV).to(BF)
+    ref = x.float().cpu() * 1.5
+    ops.scale_rows(x, 64, 1.5)
+    assert torch.equal(x.cpu(), ref.to(BF))
+    xf = torch.randn(4, 7, 80, device=DEV)
+    o = torch.empty(3 * 28, 128, device=DEV, dtype=BF)
+    ops.latent_to_input(xf, o, 3)
+    oc = o.cpu().float()
+    assert torch.equal(oc[:, 80:], torch.zeros(84, 48))
+    assert torch.equal(oc[56:84, :80], xf.cpu().reshape(28, 80).to(BF).float())
