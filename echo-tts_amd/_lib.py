@@ -51,6 +51,7 @@ class StepArgs(C.Structure):
 # name -> (restype, argtypes); must match include/echo_hip.h exactly
 SIGNATURES = {
     "echo_gemm": (i32, [C.POINTER(GemmArgs), vp]),
+    "echo_gemm_pick_tile": (i32, [i32, i32, i32, i32]),
     "echo_attention": (i32, [C.POINTER(AttnArgs), vp]),
     "echo_rmsnorm": (i32, [i32, vp, i64, vp, vp, i64, i32, i32, f32, vp]),
     "echo_adaln_modulate": (i32, [i32, vp, vp, i32, i32, vp, vp, i32, i64, f32, vp]),

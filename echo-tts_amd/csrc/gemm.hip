@@ -314,6 +314,10 @@ int launch_bf16(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 
 }  // namespace
 
+extern "C" int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch) {
+  return pick_tile(M, N, K, batch);
+}
+
 extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   if (!a || !a->A || !a->W || !a->C) return ECHO_EINVAL;
   if (a->M <= 0 || a->N <= 0 || a->K <= 0 || a->batch <= 0) return ECHO_ESHAPE;

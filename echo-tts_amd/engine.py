@@ -149,15 +149,17 @@ class CFGPlan:
                 self._scale_speaker(1.0 / self.kv_scale)
 
     def run(self, use_graph: bool) -> torch.Tensor:
-        if use_graph and self.runs > 0:
-            if self.graph is None:
+        """Eager on the first call (this also loads every kernel before any capture),
+        then capture the loop once (capture executes nothing) and replay it afterwards."""
+        if use_graph and self.graph is not None:
+            self.graph.replay()
+        else:
+            self.loop()
+            if use_graph:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     self.loop()
                 self.graph = g
-            self.graph.replay()
-        else:
-            self.loop()
         self.runs += 1
         return self.x
 

@@ -209,6 +209,7 @@ def sample_euler_cfg_independent_guidances(
                              speaker_kv_max_layers=speaker_kv_max_layers, speaker_kv_min_t=speaker_kv_min_t)
 
 
+@torch.inference_mode()
 def sample_with_noise(model, speaker_latent, speaker_mask, text_input_ids, text_mask, noise, *, num_steps,
                       cfg_scale_text, cfg_scale_speaker, cfg_min_t, cfg_max_t, truncation_factor=None,
                       rescale_k=None, rescale_sigma=None, speaker_kv_scale=None, speaker_kv_max_layers=None,

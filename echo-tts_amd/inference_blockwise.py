@@ -44,6 +44,7 @@ def sample_blockwise_euler_cfg_independent_guidances(
                                 continuation_latent=continuation_latent)
 
 
+@torch.inference_mode()
 def blockwise_with_noise(model, speaker_latent, speaker_mask, text_input_ids, text_mask,
                          noise: Callable[[tuple], torch.Tensor], block_sizes: List[int], *, num_steps,
                          cfg_scale_text, cfg_scale_speaker, cfg_min_t, cfg_max_t, truncation_factor=None,

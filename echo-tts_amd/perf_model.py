@@ -1,0 +1,94 @@
+"""Algorithmic work model of the sampling path and GEMM-launch
+instrumentation used by bench.py for the roofline numbers."""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence
+
+import torch
+
+from .config import EchoConfig
+
+AUDIO_SECONDS_PER_LATENT = 2048 / 44100.0  # inference.py:263 (AE_DOWNSAMPLE_FACTOR) at 44.1 kHz
+PEAK_BF16_TFLOPS = 2500.0                  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def gemm_flops_per_token(cfg: EchoConfig) -> int:
+    """G_tok = 2·L·(5D² + 3DF) + 2·2·80·D (decoder GEMMs per token per row-forward)."""
+    D, F, L = cfg.model_size, cfg.intermediate_size, cfg.num_layers
+    return 2 * L * (5 * D * D + 3 * D * F) + 2 * 2 * cfg.latent_size * D
+
+
+def sampler_flops(cfg: EchoConfig, N: int, steps_cfg: int, steps_plain: int, text_valid: Sequence[int],
+                  spk_valid: Sequence[int]) -> Dict[str, float]:
+    """Algorithmic FLOPs of one sampler call, summed over prompts (valid keys/tokens only)."""
+    D, L = cfg.model_size, cfg.num_layers
+    g_tok = gemm_flops_per_token(cfg)
+    a_key = 4 * D * L
+    De, Fe, Le = cfg.text_model_size, cfg.text_intermediate_size, cfg.text_num_layers
+    enc_tok = 2 * Le * (5 * De * De + 3 * De * Fe)
+    out = {"gemm": 0.0, "attention": 0.0, "setup": 0.0, "cond": 0.0}
+    for tv, sv in zip(text_valid, spk_valid):
+        rows = 3 * steps_cfg + steps_plain
+        keys = steps_cfg * ((N + tv + sv) + (N + sv) + (N + tv)) + steps_plain * (N + tv + sv)
+        out["gemm"] += rows * N * g_tok
+        out["attention"] += N * a_key * keys
+        out["setup"] += enc_tok * (tv + sv) + 2 * 2 * De * D * L * (tv + sv)
+        out["setup"] += 4 * De * Le * (tv * tv + sv * (sv + 1) / 2)
+    S = steps_cfg + steps_plain
+    r = cfg.adaln_rank
+    out["cond"] = S * 2 * (cfg.timestep_embed_size * D + D * D + 3 * D * D + 2 * L * 3 * 2 * D * r)
+    out["total"] = sum(out.values())
+    return out
+
+
+class GemmTimer:
+    """Wraps ops.gemm: HIP events around every launch of one tile config on the launch
+    stream, plus its algorithmic FLOPs (2·M·N·K·batch) — for roofline.achieved."""
+
+    def __init__(self, tile_filter=None):
+        self.records: List = []
+        self.tile_filter = tile_filter
+        self._orig = None
+
+    def __enter__(self):
+        from . import ops
+        from . import _lib
+
+        self._orig = ops.gemm
+        timer = self
+
+        def wrapped(a, w, out=None, **kw):
+            M, K = a.shape[-2], a.shape[-1]
+            N = w.shape[-2]
+            batch = max(a.shape[0] if a.dim() == 3 else 1, w.shape[0] if w.dim() == 3 else 1)
+            tile = kw.get("tile", 0) or _lib.load().echo_gemm_pick_tile(M, N, K, batch)
+            if timer.tile_filter is not None and tile not in timer.tile_filter:
+                return timer._orig(a, w, out, **kw)
+            s = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            r = timer._orig(a, w, out, **kw)
+            e1.record(s)
+            timer.records.append((e0, e1, 2.0 * M * N * K * batch, tile, (M, N, K, batch)))
+            return r
+
+        ops.gemm = wrapped
+        return self
+
+    def __exit__(self, *exc):
+        from . import ops
+        ops.gemm = self._orig
+
+    def summary(self) -> Dict[str, float]:
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b, *_ in self.records]
+        fl = [r[2] for r in self.records]
+        n = len(ms)
+        if n == 0:
+            return {"launches": 0}
+        avg_ms = sum(ms) / n
+        avg_fl = sum(fl) / n
+        return {"launches": n, "avg_ms": avg_ms, "avg_flop": avg_fl,
+                "tflops": avg_fl / (avg_ms * 1e-3) / 1e12}

@@ -62,6 +62,9 @@ typedef struct {
  * 118-122,177-197,303-305,443,532-540,557) plus the fused elementwise tails above. */
 int echo_gemm(const EchoGemmArgs* args, void* stream);
 
+/* Tile configuration echo_gemm picks for a shape when args->tile == 0 (1..5). */
+int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch);
+
 /* One key/value segment of the joint attention (model.py:246-253): rows of
  * `len[row]` valid tokens (prefix), head h at element offset h*128. */
 typedef struct {

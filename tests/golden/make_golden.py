@@ -239,6 +239,25 @@ def gen_full(ref_model, ref_inf):
     with open(os.path.join(HERE, "full_c1_fp32.json"), "w") as f:
         json.dump({"kw": kw, "seq": 64, "seed": 0, "time_s": time.time() - t0}, f, indent=1)
     print("C1 done", time.time() - t0)
+
+    # fp32 reference truth of the C2-nfe forwards (same weights, same inputs as the bf16 ones below)
+    ids2, tm2 = SY.text_inputs(1)
+    spk2, sm2 = SY.speaker_inputs(1)
+    x2 = torch.randn((1, 640, 80), generator=torch.Generator().manual_seed(0))
+    ts = torch.linspace(1.0, 0.0, 41) * 0.999
+    f32 = {}
+    with torch.inference_mode():
+        kvt = m.get_kv_cache_text(ids2, tm2)
+        kvs = m.get_kv_cache_speaker(spk2)
+        f32["kv_text.0.k.head"] = kvt[0][0][:, :64].contiguous()
+        f32["kv_speaker.0.k"] = kvs[0][0].contiguous()
+        ft = torch.cat([tm2, torch.zeros_like(tm2), tm2])
+        fs = torch.cat([sm2, sm2, torch.zeros_like(sm2)])
+        f32["v_cfg"] = m(x=torch.cat([x2, x2, x2]), t=torch.ones(3) * ts[0].to(torch.bfloat16).float(),
+                         text_mask=ft, speaker_mask=fs, kv_cache_text=ref_inf._concat_kv_caches(kvt, kvt, kvt),
+                         kv_cache_speaker=ref_inf._concat_kv_caches(kvs, kvs, kvs))
+        f32["v_plain"] = m(x=x2, t=torch.ones(1) * ts[30].to(torch.bfloat16).float(), text_mask=tm2,
+                           speaker_mask=sm2, kv_cache_text=kvt, kv_cache_speaker=kvs)
     del m
 
     # F-C2-nfe: bf16, one 3-row CFG forward at N=640, T=768 (388 valid), P=160; plus a 1-row forward
@@ -265,6 +284,8 @@ def gen_full(ref_model, ref_inf):
         v1 = m(x=x.to(torch.bfloat16), t=(torch.ones(1) * ts[30]).to(torch.bfloat16), text_mask=tmask,
                speaker_mask=smask, kv_cache_text=kvt, kv_cache_speaker=kvs)
         out["v_plain"] = v1
+    for k, v in f32.items():
+        out["fp32." + k] = v
     save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(HERE, "full_c2_nfe_bf16.safetensors"))
     cks = {k: W.checksum(v) for k, v in state.items() if k.startswith("blocks.0.") or k.startswith("cond")}
     with open(os.path.join(HERE, "full_c2_nfe_bf16.json"), "w") as f:

@@ -196,28 +196,51 @@ def full_bf16():
     return EchoDiTHip(E.FULL, S, device=DEV, dtype=torch.bfloat16)
 
 
-def test_full_c2_nfe_bf16(full_bf16):
-    """Production shapes (N=640, T=768/388 valid, P=160): one 3-row CFG NFE and one plain NFE."""
-    m = full_bf16
+def _c2_inputs():
     g = {k: v.to(DEV) for k, v in load_golden("full_c2_nfe_bf16").items()}
-    tm, sm = g["text_mask"], g["speaker_mask"]
+    return g, g["text_mask"], g["speaker_mask"]
+
+
+def _c2_forwards(m, g, tm, sm, dt):
     kt = m.get_kv_cache_text(g["text_ids"], tm)
-    ks = m.get_kv_cache_speaker(g["speaker_latent"].to(torch.bfloat16))
-    assert rel_l2(kt[0][0][:, :64].cpu(), g["kv_text.0.k.head"].cpu()) < NFE_TOL
-    assert rel_l2(kt[23][1][:, :64].cpu(), g["kv_text.23.v.head"].cpu()) < NFE_TOL
-    assert rel_l2(ks[0][0].cpu(), g["kv_speaker.0.k"].cpu()) < NFE_TOL
-    assert rel_l2(ks[23][1].cpu(), g["kv_speaker.23.v"].cpu()) < NFE_TOL
+    ks = m.get_kv_cache_speaker(g["speaker_latent"].to(dt))
     ts = torch.linspace(1.0, 0.0, 41) * 0.999
     x = g["x"]
-    v3 = m(x=torch.cat([x, x, x]).to(torch.bfloat16), t=(torch.ones(3) * ts[0]).to(torch.bfloat16).to(DEV),
-           text_mask=torch.cat([tm, torch.zeros_like(tm), tm]), speaker_mask=torch.cat([sm, sm, torch.zeros_like(sm)]),
-           kv_cache_text=cat3(kt), kv_cache_speaker=cat3(ks))
-    e3 = rel_l2(v3.cpu(), g["v_cfg"].cpu())
-    v1 = m(x=x.to(torch.bfloat16), t=(torch.ones(1) * ts[30]).to(torch.bfloat16).to(DEV), text_mask=tm,
-           speaker_mask=sm, kv_cache_text=kt, kv_cache_speaker=ks)
-    e1 = rel_l2(v1.cpu(), g["v_plain"].cpu())
-    print(f"[full C2] NFE rel-L2: cfg {e3:.2e}, plain {e1:.2e}")
-    assert e3 < NFE_TOL and e1 < NFE_TOL
+    t0 = (torch.ones(3) * ts[0]).to(torch.bfloat16).to(dt).to(DEV)
+    t30 = (torch.ones(1) * ts[30]).to(torch.bfloat16).to(dt).to(DEV)
+    v3 = m(x=torch.cat([x, x, x]).to(dt), t=t0, text_mask=torch.cat([tm, torch.zeros_like(tm), tm]),
+           speaker_mask=torch.cat([sm, sm, torch.zeros_like(sm)]), kv_cache_text=cat3(kt), kv_cache_speaker=cat3(ks))
+    v1 = m(x=x.to(dt), t=t30, text_mask=tm, speaker_mask=sm, kv_cache_text=kt, kv_cache_speaker=ks)
+    return {"kv_text.0.k.head": kt[0][0][:, :64], "kv_speaker.0.k": ks[0][0], "v_cfg": v3, "v_plain": v1}
+
+
+def test_full_c2_nfe_bf16(full_bf16):
+    """Production shapes (N=640, T=768/388 valid, P=160), bf16.
+
+    With random weights the 14-layer encoders amplify bf16 rounding: the
+    reference's own bf16 text KV is ~1.4e-2 from its fp32 result.
+    Gate: our bf16 must be no further from the reference's fp32 truth than the
+    reference's bf16 is (x1.25 + 1e-3), for the KV caches and both NFE outputs."""
+    g, tm, sm = _c2_inputs()
+    got = _c2_forwards(full_bf16, g, tm, sm, torch.bfloat16)
+    for k, v in got.items():
+        ref16, ref32 = g[k].cpu(), g["fp32." + k].cpu()
+        e_ours, e_ref, e_pair = rel_l2(v.cpu(), ref32), rel_l2(ref16, ref32), rel_l2(v.cpu(), ref16)
+        print(f"[full C2 bf16] {k}: ours-vs-fp32 {e_ours:.2e}, ref16-vs-fp32 {e_ref:.2e}, ours-vs-ref16 {e_pair:.2e}")
+        assert e_ours <= 1.25 * e_ref + 1e-3, k
+
+
+def test_full_c2_nfe_fp32():
+    """The same production-shape NFEs in fp32 mode against the reference's fp32 outputs."""
+    S = W.synthetic_state_dict(E.FULL, dtype=torch.float32, include_latent=False)
+    m = EchoDiTHip(E.FULL, S, device=DEV, dtype=torch.float32)
+    del S
+    g, tm, sm = _c2_inputs()
+    got = _c2_forwards(m, g, tm, sm, torch.float32)
+    for k, v in got.items():
+        e = rel_l2(v.cpu(), g["fp32." + k].cpu())
+        print(f"[full C2 fp32] {k}: rel-L2 {e:.2e}")
+        assert e < 1e-4, k
 
 
 def test_full_c1_fp32():
