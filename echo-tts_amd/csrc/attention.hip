@@ -31,16 +31,24 @@ __device__ __forceinline__ int remap_xcd(int bid, int nwg) {
 constexpr int QB = 128;  // queries per workgroup
 constexpr int KT = 64;   // keys per tile
 
+struct SegInfo {
+  const bf16_t* kb;
+  const bf16_t* vb;
+  int64_t ld;
+  int kend, causal, first;  // first = index of the segment's first tile in the flat tile list
+};
+
 __global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[KT * 128];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[KT * 128];
+  // [buffer][K | V][64 keys x 128] — one array (keeps hipcc from draining DMA before ds_reads)
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KT * 128];
 
   const int nqb = (a.n_q + QB - 1) / QB;
   const int L = remap_xcd(blockIdx.x, gridDim.x);
   const int qb = L % nqb;
   const int head = (L / nqb) % a.heads;
   const int row = L / (nqb * a.heads);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h2 = lane >> 5, ql = lane & 31;
   const int q0 = qb * QB;
   const int qi = q0 + w * 32 + ql;
@@ -51,6 +59,57 @@ __global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
 #pragma unroll
   for (int ds = 0; ds < 8; ++ds) qf[ds] = *(const bf16x8*)(qp + 16 * ds + 8 * h2);
 
+  // flat list of 64-key tiles over the (up to 4) segments; per-segment fields are kept in
+  // named scalars (no runtime-indexed arrays: those go to scratch)
+  SegInfo s0{}, s1{}, s2{}, s3{};
+  int ntiles = 0;
+  auto init_seg = [&](int sg, SegInfo& d) {
+    d.first = ntiles;
+    if (sg < a.nseg && a.seg[sg].k) {
+      const EchoKVSegment& S = a.seg[sg];
+      const int len = S.len ? S.len[row] : S.capacity;
+      int kend = min(len, S.capacity);
+      if (S.causal) kend = min(kend, q0 + QB);
+      kend = max(kend, 0);
+      const int b = row % S.batch_mod;
+      d.kb = (const bf16_t*)S.k + b * S.ld_batch + head * 128;
+      d.vb = (const bf16_t*)S.v + b * S.ld_batch + head * 128;
+      d.ld = S.ld_tok;
+      d.kend = kend;
+      d.causal = S.causal;
+      ntiles += (kend + KT - 1) / KT;
+    }
+  };
+  init_seg(0, s0);
+  init_seg(1, s1);
+  init_seg(2, s2);
+  init_seg(3, s3);
+  auto pick = [&](int ti) -> SegInfo {
+    return ti >= s3.first && s3.kend > 0 ? s3 : ti >= s2.first && s2.kend > 0 ? s2
+         : ti >= s1.first && s1.kend > 0 ? s1 : s0;
+  };
+
+  // DMA of tile ti into buffer `buf`: 64 rows x 256 B for K and V = 32 wave-instructions
+  // of 1 KiB (4 rows each); lane-linear LDS image, XOR swizzle applied on the source chunk.
+  const int dr = lane >> 4, dp = lane & 15;
+  auto dma_tile = [&](int ti, int buf) {
+    const SegInfo d = pick(ti);
+    const int t0 = (ti - d.first) * KT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (i * 4 + w) * 4 + dr;  // tile row 0..63 written by this lane
+      const int64_t tok = min(t0 + r, d.kend - 1);
+      const int c = dp ^ swz(r);
+      const int dst = ((i * 4 + w) * 4) * 128;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(d.kb + tok * d.ld + c * 8),
+                                       (__attribute__((address_space(3))) void*)(lds + (buf * 2) * KT * 128 + dst),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(d.vb + tok * d.ld + c * 8),
+                                       (__attribute__((address_space(3))) void*)(lds + (buf * 2 + 1) * KT * 128 + dst),
+                                       16, 0, 0);
+    }
+  };
+
   f32x16 o[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
@@ -58,111 +117,105 @@ __global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
     for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
   const float sl2 = a.scale * 1.4426950408889634f;
-
-  // transposed-read lane geometry (ds_read_b64_tr_b16: 16-lane groups, 4 rows x 16 cols)
   const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
 
-#pragma unroll
-  for (int sg = 0; sg < 4; ++sg) {
-    if (sg >= a.nseg) break;
-    const EchoKVSegment S = a.seg[sg];
-    if (!S.k) continue;
-    const int len = S.len ? S.len[row] : S.capacity;
-    int kend = min(len, S.capacity);
-    if (S.causal) kend = min(kend, q0 + QB);
-    if (kend <= 0) continue;
-    const int b = row % S.batch_mod;
-    const bf16_t* kb = (const bf16_t*)S.k + b * S.ld_batch + head * 128;
-    const bf16_t* vb = (const bf16_t*)S.v + b * S.ld_batch + head * 128;
-    for (int t0 = 0; t0 < kend; t0 += KT) {
-      // ---- stage the K and V tiles (register-staged, 16 B per lane per row chunk)
-      u32x4 kr[4], vr[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int idx = i * 256 + tid, r = idx >> 4, c = idx & 15;
-        const int64_t tok = min(t0 + r, kend - 1);
-        kr[i] = *(const u32x4*)(kb + tok * S.ld_tok + c * 8);
-        vr[i] = *(const u32x4*)(vb + tok * S.ld_tok + c * 8);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int idx = i * 256 + tid, r = idx >> 4, c = idx & 15;
-        const int off = r * 128 + ((c ^ swz(r)) * 8);
-        *(u32x4*)(Ks + off) = kr[i];
-        *(u32x4*)(Vs + off) = vr[i];
-      }
-      __syncthreads();
+  if (ntiles > 0) dma_tile(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
-      // ---- S^T = K . Q^T for two 32-key sub-tiles
-      f32x16 st[2];
+  for (int ti = 0; ti < ntiles; ++ti) {
+    const int cur = ti & 1;
+    if (ti + 1 < ntiles) dma_tile(ti + 1, cur ^ 1);  // lands while this tile computes
+    const bf16_t* Ks = lds + (cur * 2) * KT * 128;
+    const bf16_t* Vs = Ks + KT * 128;
+    const SegInfo d = pick(ti);
+    const int t0 = (ti - d.first) * KT;
+    const int kend = d.kend;
+    const bool full = (t0 + KT <= kend) && !d.causal;
+
+    // ---- S^T = K . Q^T for two 32-key sub-tiles
+    f32x16 st[2];
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) st[kk][r] = 0.f;
-        const int kr_ = kk * 32 + ql;
+      for (int r = 0; r < 16; ++r) st[kk][r] = 0.f;
+      const int kr_ = kk * 32 + ql;
 #pragma unroll
-        for (int ds = 0; ds < 8; ++ds) {
-          const int c = 2 * ds + h2;
-          const bf16x8 kf = *(const bf16x8*)(Ks + kr_ * 128 + ((c ^ swz(kr_)) * 8));
-          st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], st[kk], 0, 0, 0);
-        }
+      for (int ds = 0; ds < 8; ++ds) {
+        const int c = 2 * ds + h2;
+        const bf16x8 kf = *(const bf16x8*)(Ks + kr_ * 128 + ((c ^ swz(kr_)) * 8));
+        st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], st[kk], 0, 0, 0);
       }
-      // ---- mask, online softmax (lane = query, registers = keys)
-      float mx = -INFINITY;
+    }
+    // ---- mask (partial tiles only), online softmax (lane = query, registers = keys)
+    float mx = -INFINITY;
+    if (full) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          st[kk][r] *= sl2;
+          mx = fmaxf(mx, st[kk][r]);
+        }
+    } else {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = t0 + kk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
-          const bool ok = key < kend && (!S.causal || key <= qi);
-          const float s = ok ? st[kk][r] * sl2 : -INFINITY;
-          st[kk][r] = s;
-          mx = fmaxf(mx, s);
+          const bool ok = key < kend && (!d.causal || key <= qi);
+          const float sv = ok ? st[kk][r] * sl2 : -INFINITY;
+          st[kk][r] = sv;
+          mx = fmaxf(mx, sv);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run, mx);
-      const float msub = m_new == -INFINITY ? 0.f : m_new;
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float msub = m_new == -INFINITY ? 0.f : m_new;
+    float psum = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = exp2f(st[kk][r] - msub);
+        st[kk][r] = pv;
+        psum += pv;
+      }
+    if (__any(m_new != m_run)) {  // otherwise alpha == 1 exactly for every lane
       const float alpha = exp2f(m_run - msub);
-      float psum = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(st[kk][r] - msub);
-          st[kk][r] = p;
-          psum += p;
-        }
-      l_run = l_run * alpha + psum;
-      m_run = m_new;
+      l_run *= alpha;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-
-      // ---- O^T += V^T . P  (P from the accumulators, V^T by transposed LDS reads)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 pf;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) pf[j] = (__bf16)st[kk][8 * s2 + j];
-          const int key0 = kk * 32 + 16 * s2 + 4 * h2;
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt) {
-            const int ch = 4 * dt + 2 * (g & 1) + (p4 >> 1);
-            const int r0 = key0 + q4, r1 = key0 + 8 + q4;
-            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s16x4*)(Vs + r0 * 128 + ((ch ^ swz(r0)) * 8) + (p4 & 1) * 4));
-            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s16x4*)(Vs + r1 * 128 + ((ch ^ swz(r1)) * 8) + (p4 & 1) * 4));
-            typedef __attribute__((ext_vector_type(8))) short s16x8;
-            const s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf, o[dt], 0, 0, 0);
-          }
-        }
     }
+    l_run += psum;
+    m_run = m_new;
+
+    // ---- O^T += V^T . P  (P from the accumulators, V^T by transposed LDS reads)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[j] = (__bf16)st[kk][8 * s2 + j];
+        const int key0 = kk * 32 + 16 * s2 + 4 * h2;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int ch = 4 * dt + 2 * (g & 1) + (p4 >> 1);
+          const int r0 = key0 + q4, r1 = key0 + 8 + q4;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(Vs + r0 * 128 + ((ch ^ swz(r0)) * 8) + (p4 & 1) * 4));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(Vs + r1 * 128 + ((ch ^ swz(r1)) * 8) + (p4 & 1) * 4));
+          typedef __attribute__((ext_vector_type(8))) short s16x8;
+          const s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf, o[dt], 0, 0, 0);
+        }
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next tile landed (this wave's share)
+    __syncthreads();                                    // ... and everyone's; buffer `cur` free
   }
 
   // ---- epilogue: normalise, round, gate, store (4 consecutive d per register group)

@@ -73,6 +73,7 @@ def kv_scale_cols(model: EchoDiTHip, max_layers: Optional[int]) -> int:
 class CFGPlan:
     """Buffers + (optional) captured graph for one (B, N, text cap, speaker cap, schedule)."""
 
+    @torch.inference_mode(False)
     def __init__(self, model: EchoDiTHip, B: int, N: int, Tc: int, Pc: int, sched: Schedule,
                  kv_scale: Optional[float], kv_max_layers: Optional[int]):
         self.m, self.B, self.N, self.Tc, self.Pc, self.sched = model, B, N, Tc, Pc, sched

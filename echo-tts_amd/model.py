@@ -106,7 +106,9 @@ class KVStore:
 class Workspace:
     """Activation buffers for R*N decoder rows (re-used across layers and steps)."""
 
+    @torch.inference_mode(False)
     def __init__(self, rows: int, cfg: EchoConfig, device, dtype):
+        # normal (non-inference) tensors: usable from inference-mode samplers and plain calls alike
         D, F = cfg.model_size, cfg.intermediate_size
         mk = lambda *s: torch.empty(s, device=device, dtype=dtype)  # noqa: E731
         self.rows = rows
@@ -266,7 +268,7 @@ class EchoDiTHip:
                            pos_mult=cfg.speaker_patch_size)
         return kv.view(B, Tc, nl, 2, H, 128)
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def text_kv(self, ids: Tensor, mask: Optional[Tensor], trim: bool = True, cap: Optional[int] = None,
                 out: Optional[Tensor] = None) -> KVStore:
         """get_kv_cache_text (model.py:606-613). trim: encode only up to the longest valid prefix
@@ -312,7 +314,7 @@ class EchoDiTHip:
         st = ops.rmsnorm(x, norm, cfg.norm_eps)
         return KVStore(self._kv_project(st, w_kv, B, Pc, latent_rope, out), [min(v, Pc) for v in valid])
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def speaker_kv(self, latent: Tensor, mask: Optional[Tensor], trim: bool = True, cap: Optional[int] = None,
                    out: Optional[Tensor] = None) -> KVStore:
         ps = self.cfg.speaker_patch_size
@@ -320,7 +322,7 @@ class EchoDiTHip:
         return self._patch_kv(latent, valid, self.speaker_enc, self.speaker_norm, self.w_kv_speaker, False, trim,
                               cap, out)
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def latent_kv(self, prefix: Tensor, valid_patches: Optional[int] = None, trim: bool = True) -> KVStore:
         if not self.has_latent:
             raise RuntimeError("model was built without the blockwise (latent) modules")
@@ -328,20 +330,20 @@ class EchoDiTHip:
         valid = None if valid_patches is None else [valid_patches] * B
         return self._patch_kv(prefix, valid, self.latent_enc, self.latent_norm, self.w_kv_latent, True, trim)
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def get_kv_cache_text(self, text_input_ids: Tensor, text_mask: Optional[Tensor]) -> List[Tuple[Tensor, Tensor]]:
         return self.text_kv(text_input_ids, text_mask, trim=False).as_list()
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def get_kv_cache_speaker(self, speaker_latent: Tensor) -> List[Tuple[Tensor, Tensor]]:
         return self.speaker_kv(speaker_latent, None, trim=False).as_list()
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def get_kv_cache_latent(self, prefix_latent: Tensor) -> List[Tuple[Tensor, Tensor]]:
         return self.latent_kv(prefix_latent, trim=False).as_list()
 
     # ------------------------------------------------------------------ conditioning table
-    @torch.inference_mode()
+    @torch.no_grad()
     def adaln_table(self, t_values: Sequence[float]) -> Tensor:
         """[S, 2L, 3, D] = (shift, round(scale+1), round(tanh(gate))) of every layer's two AdaLNs
         for each timestep (cond_module + LowRankAdaLN, model.py:27-43,64-81,532-538,583-584).
@@ -421,7 +423,7 @@ class EchoDiTHip:
         return ws.v[:M]
 
     # ------------------------------------------------------------------ generic forward (API)
-    @torch.inference_mode()
+    @torch.no_grad()
     def forward(self, x: Tensor, t: Tensor, text_mask: Tensor, speaker_mask: Tensor,
                 kv_cache_text: List[Tuple[Tensor, Tensor]], kv_cache_speaker: List[Tuple[Tensor, Tensor]],
                 start_pos: Optional[int] = None, kv_cache_latent: Optional[List[Tuple[Tensor, Tensor]]] = None

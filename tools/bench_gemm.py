@@ -1,0 +1,74 @@
+"""GEMM microbenchmark on the decoder's production shapes (B=16 CFG / plain rows).
+
+Interleaved rounds of every tile config in one process (cdna_hip_programming.md §5.4
+rule 24), random operands, HIP events on the launch stream. Also checks that each
+config's output is bitwise equal to config 1 (same K accumulation order).
+    python tools/bench_gemm.py [--tiles 1,6] [--rounds 5]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import echo_tts_amd  # noqa: E402
+from echo_tts_amd import _lib as L  # noqa: E402
+from echo_tts_amd import ops  # noqa: E402
+
+SHAPES = [  # name, M, N, K, epilogue
+    ("qkvg M30720", 30720, 8192, 2048, L.EPI_STORE),
+    ("wo   M30720", 30720, 2048, 2048, L.EPI_RESID),
+    ("w13  M30720", 30720, 11776, 2048, L.EPI_SWIGLU),
+    ("w2   M30720", 30720, 2048, 5888, L.EPI_RESID),
+    ("qkvg M10240", 10240, 8192, 2048, L.EPI_STORE),
+    ("wo   M10240", 10240, 2048, 2048, L.EPI_RESID),
+    ("w13  M10240", 10240, 11776, 2048, L.EPI_SWIGLU),
+    ("w2   M10240", 10240, 2048, 5888, L.EPI_RESID),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tiles", default="1,6")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    tiles = [int(t) for t in args.tiles.split(",")]
+    dev = "cuda"
+    torch.manual_seed(0)
+    for name, M, N, K, epi in SHAPES:
+        a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+        nout = N // 2 if epi == L.EPI_SWIGLU else N
+        aux = torch.randn(M, nout, device=dev).to(torch.bfloat16)
+        gate = torch.randn(nout, device=dev).to(torch.bfloat16) if epi == L.EPI_RESID else None
+        outs = {}
+        for t in tiles:
+            o = aux.clone() if epi == L.EPI_RESID else torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
+            ops.gemm(a, w, out=o, epilogue=epi, aux=o if epi == L.EPI_RESID else None, gate=gate, tile=t)
+            outs[t] = o
+        base = outs[tiles[0]]
+        same = {t: bool(torch.equal(outs[t], base)) for t in tiles}
+        times = {t: [] for t in tiles}
+        out = torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
+        for _ in range(args.rounds):
+            for t in tiles:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.iters):
+                    ops.gemm(a, w, out=out, epilogue=epi, aux=aux if epi == L.EPI_RESID else None, gate=gate,
+                             tile=t)
+                e1.record()
+                torch.cuda.synchronize()
+                times[t].append(e0.elapsed_time(e1) / args.iters)
+        fl = 2.0 * M * N * K
+        line = f"{name} N={N:5d} K={K:4d}:"
+        for t in tiles:
+            ms = sorted(times[t])[len(times[t]) // 2]
+            line += f"  t{t} {ms * 1e3:7.1f}us {fl / ms / 1e9:6.0f}TF{'' if same[t] else ' MISMATCH'}"
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()
