@@ -1,0 +1,91 @@
+"""The C ABI library: builds for gfx950, loads without a GPU, exports every symbol that
+include/echo_hip.h declares, and the ctypes structs match the C layouts (gcc offsetof)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+import echo_tts_amd  # noqa: F401
+from echo_tts_amd import _lib as L
+from echo_tts_amd import build as B
+
+HEADER = os.path.join(REPO, "include", "echo_hip.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    B.build(verbose=False)
+    return L.load()
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(echo_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_every_declared_symbol_is_exported_and_bound(lib):
+    names = declared_functions()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(lib, n), f"{n} not exported by libecho_hip.so"
+        assert n in L.SIGNATURES, f"{n} not bound in _lib.SIGNATURES"
+    assert set(L.SIGNATURES) == set(names)
+    assert lib.echo_version().decode().startswith("echo_hip gfx950")
+
+
+def test_library_targets_gfx950():
+    """The fat binary embedded in the .so carries a gfx950 code object (and no other target)."""
+    B.build(verbose=False)
+    blob = open(B.OUT, "rb").read()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-f]+)", blob))
+    assert targets == {b"gfx950"}, targets
+
+
+STRUCTS = {
+    "EchoGemmArgs": L.GemmArgs,
+    "EchoKVSegment": L.KVSegment,
+    "EchoAttnArgs": L.AttnArgs,
+    "EchoStepArgs": L.StepArgs,
+}
+
+
+def test_struct_layouts_match_header(tmp_path):
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
+    for cname, cls in STRUCTS.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
+    got = {}
+    for ln in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        s, f, v = ln.split()
+        got[(s, f)] = int(v)
+    for cname, cls in STRUCTS.items():
+        assert got[(cname, "size")] == C.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert got[(cname, f)] == getattr(cls, f).offset, (cname, f)
+
+
+def test_ops_refuse_cpu_tensors(lib):
+    import torch
+    from echo_tts_amd import ops
+    a = torch.zeros(4, 64, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ops.gemm(a, a)
+
+
+def test_model_refuses_cpu_device(lib):
+    import torch
+    import echo_tts_amd as E
+    from echo_tts_amd.model import EchoDiTHip
+    with pytest.raises(RuntimeError, match="HIP device only"):
+        EchoDiTHip(E.tiny(), {}, device="cpu", dtype=torch.bfloat16)
