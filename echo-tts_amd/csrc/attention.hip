@@ -28,6 +28,20 @@ __device__ __forceinline__ int remap_xcd(int bid, int nwg) {
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 }
 
+// LDS-DMA (global_load_lds_dwordx4) issued through inline asm: hipcc does not see it, so it
+// cannot insert a conservative vmcnt(0) in front of the ds_reads of the OTHER buffer (it did
+// for the V transposed reads). Completion is waited for explicitly (vmcnt(0) + barrier at the
+// end of each tile). M0 is saved/restored inside the statement (cdna_hip_programming.md §5.7).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_addr) : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 constexpr int QB = 128;  // queries per workgroup
 constexpr int KT = 64;   // keys per tile
 
@@ -58,6 +72,10 @@ __global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
   bf16x8 qf[8];
 #pragma unroll
   for (int ds = 0; ds < 8; ++ds) qf[ds] = *(const bf16x8*)(qp + 16 * ds + 8 * h2);
+  // consume Q here so hipcc waits for it once, not inside the tile loop (where its counted
+  // waits would land on the asm DMA of the next tile)
+#pragma unroll
+  for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));
 
   // flat list of 64-key tiles over the (up to 4) segments; per-segment fields are kept in
   // named scalars (no runtime-indexed arrays: those go to scratch)
@@ -101,12 +119,10 @@ __global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
       const int64_t tok = min(t0 + r, d.kend - 1);
       const int c = dp ^ swz(r);
       const int dst = ((i * 4 + w) * 4) * 128;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(d.kb + tok * d.ld + c * 8),
-                                       (__attribute__((address_space(3))) void*)(lds + (buf * 2) * KT * 128 + dst),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(d.vb + tok * d.ld + c * 8),
-                                       (__attribute__((address_space(3))) void*)(lds + (buf * 2 + 1) * KT * 128 + dst),
-                                       16, 0, 0);
+      const uint32_t kdst = __builtin_amdgcn_readfirstlane(lds_addr_of(lds + (buf * 2) * KT * 128 + dst));
+      const uint32_t vdst = __builtin_amdgcn_readfirstlane(lds_addr_of(lds + (buf * 2 + 1) * KT * 128 + dst));
+      glds16(d.kb + tok * d.ld + c * 8, kdst);
+      glds16(d.vb + tok * d.ld + c * 8, vdst);
     }
   };
 
@@ -147,42 +163,38 @@ __global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
         st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], st[kk], 0, 0, 0);
       }
     }
-    // ---- mask (partial tiles only), online softmax (lane = query, registers = keys)
+    // ---- mask (partial tiles only), online softmax (lane = query, registers = keys).
+    // The running max is kept on RAW scores (scale > 0 preserves the argmax); one FMA per score
+    // forms the exp2 argument s*c - m*c; raw v_exp_f32 (results < 2^-126 flush to 0).
     float mx = -INFINITY;
-    if (full) {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          st[kk][r] *= sl2;
-          mx = fmaxf(mx, st[kk][r]);
-        }
-    } else {
+    if (!full) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = t0 + kk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
           const bool ok = key < kend && (!d.causal || key <= qi);
-          const float sv = ok ? st[kk][r] * sl2 : -INFINITY;
-          st[kk][r] = sv;
-          mx = fmaxf(mx, sv);
+          st[kk][r] = ok ? st[kk][r] : -INFINITY;
         }
     }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) mx = fmaxf(mx, fmaxf(st[kk][r], st[kk][r + 1]));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, mx);
-    const float msub = m_new == -INFINITY ? 0.f : m_new;
+    const float msc = m_new == -INFINITY ? 0.f : -m_new * sl2;
     float psum = 0.f;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float pv = exp2f(st[kk][r] - msub);
+        const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(st[kk][r], sl2, msc));
         st[kk][r] = pv;
         psum += pv;
       }
     if (__any(m_new != m_run)) {  // otherwise alpha == 1 exactly for every lane
-      const float alpha = exp2f(m_run - msub);
+      const float alpha = __builtin_amdgcn_exp2f(__builtin_fmaf(m_run, sl2, msc));
       l_run *= alpha;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)

@@ -98,6 +98,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
     float v[8];
     load8(stg + row * TNo + ((c ^ (row & (CH - 1))) * 8), v);
     if (m >= M || n >= Nout) continue;
+    if (ep.epi == 99) { asm volatile("" ::"v"(v[0]), "v"(v[7])); continue; }
     if (ep.epi == ECHO_EPI_RESID) {
       float x[8];
       load8((const bf16_t*)ep.aux + z * ep.stride_aux + (int64_t)m * ep.ld_aux + n, x);
@@ -368,7 +369,16 @@ gemm_bf16_pp_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   if (wm == 0) pp_barrier();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  gemm_epilogue<TM, TN, FM, FN>(acc, lds, wid, wm, wn, lane, m0, n0, M, N, z, Cv, ldc, sC, ep);
+  if (ABL & 8) {  // timing ablation: keep acc live, no epilogue
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+  Epi e2 = ep;
+  if (ABL & 4) e2.epi = 99;  // timing ablation: stage 2 loads/stores skipped
+  gemm_epilogue<TM, TN, FM, FN>(acc, lds, wid, wm, wn, lane, m0, n0, M, N, z, Cv, ldc, sC, e2);
 }
 
 // ----------------------------------------------------------------------------- fp32 (parity mode)
@@ -523,6 +533,9 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
     case 7: return launch_pp<1>(a, ep, s);
     case 8: return launch_pp<2>(a, ep, s);
     case 9: return launch_pp<3>(a, ep, s);
+    case 10: return launch_pp<4>(a, ep, s);
+    case 11: return launch_pp<8>(a, ep, s);
+    case 12: return launch_pp<11>(a, ep, s);
     default: return ECHO_EINVAL;
   }
 }

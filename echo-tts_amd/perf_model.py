@@ -71,7 +71,11 @@ class GemmTimer:
             e0.record(s)
             r = timer._orig(a, w, out, **kw)
             e1.record(s)
-            timer.records.append((e0, e1, 2.0 * M * N * K * batch, tile, (M, N, K, batch)))
+            nout = N // 2 if kw.get("epilogue", 0) == _lib.EPI_SWIGLU else N
+            osz = 4 if kw.get("epilogue", 0) == _lib.EPI_F32OUT else 2
+            byts = 2 * (M * K * (a.shape[0] if a.dim() == 3 else 1) + N * K * (w.shape[0] if w.dim() == 3 else 1)) \
+                + osz * M * nout * batch + (2 * M * nout * batch if kw.get("aux") is not None else 0)
+            timer.records.append((e0, e1, 2.0 * M * N * K * batch, tile, (M, N, K, batch), byts))
             return r
 
         ops.gemm = wrapped
@@ -91,4 +95,5 @@ class GemmTimer:
         avg_ms = sum(ms) / n
         avg_fl = sum(fl) / n
         return {"launches": n, "avg_ms": avg_ms, "avg_flop": avg_fl,
+                "avg_bytes": sum(r[5] for r in self.records) / n,
                 "tflops": avg_fl / (avg_ms * 1e-3) / 1e12}

@@ -1,0 +1,49 @@
+"""Attention microbenchmark on the decoder's CFG shape (B=16 -> 48 rows, N=640, H=16,
+text 388/768, speaker 160): real layout vs every row reading row 0's K/V (cache-resident),
+to separate memory-bound from compute-bound behaviour."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import echo_tts_amd  # noqa: E402
+from echo_tts_amd import ops  # noqa: E402
+
+
+def timeit(fn, iters=10, rounds=5):
+    ts = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / iters)
+    return sorted(ts)[len(ts) // 2]
+
+
+def main():
+    dev = "cuda"
+    B, N, H, T, P = 16, 640, 16, 448, 160
+    for R, tl_c, sl_c in ((3 * B, [388] * B + [0] * B + [388] * B, [160] * 2 * B + [0] * B),
+                          (B, [388] * B, [160] * B)):
+        qkvg = (torch.randn(R, N, 4, H, 128, device=dev)).to(torch.bfloat16)
+        kt = torch.randn(B, T, 24, 2, H, 128, device=dev).to(torch.bfloat16)[:, :, 3]
+        ks = torch.randn(B, P, 24, 2, H, 128, device=dev).to(torch.bfloat16)[:, :, 3]
+        tl = torch.tensor(tl_c, dtype=torch.int32, device=dev)
+        sl = torch.tensor(sl_c, dtype=torch.int32, device=dev)
+        out = torch.empty(R, N, H, 128, device=dev, dtype=torch.bfloat16)
+        keys = sum(N + t + s for t, s in zip(tl_c, sl_c))
+        fl = 4.0 * N * keys * 128 * H
+        for name, bm_self, bm_c in (("real", None, B), ("shared-kv", 1, 1)):
+            segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2], batch_mod=bm_self),
+                    ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=bm_c),
+                    ops.Segment(ks[:, :, 0], ks[:, :, 1], lens=sl, batch_mod=bm_c)]
+            ms = timeit(lambda: ops.attention(qkvg[:, :, 0], segs, out=out, gate=qkvg[:, :, 3]))
+            print(f"R={R:3d} {name:10s} {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

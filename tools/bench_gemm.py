@@ -28,16 +28,36 @@ SHAPES = [  # name, M, N, K, epilogue
 ]
 
 
+def timeit_fill(out, args):
+    ts = []
+    for _ in range(args.rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iters):
+            out.fill_(1.0)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / args.iters)
+    return sorted(ts)[len(ts) // 2]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", default="1,6")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--shapes", default=None, help="M,N,K[,epi];... overrides the production list")
     args = ap.parse_args()
+    shapes = SHAPES
+    if args.shapes:
+        shapes = []
+        for sp in args.shapes.split(";"):
+            v = [int(x) for x in sp.split(",")]
+            shapes.append((f"M{v[0]}", v[0], v[1], v[2], v[3] if len(v) > 3 else L.EPI_STORE))
     tiles = [int(t) for t in args.tiles.split(",")]
     dev = "cuda"
     torch.manual_seed(0)
-    for name, M, N, K, epi in SHAPES:
+    for name, M, N, K, epi in shapes:
         a = torch.randn(M, K, device=dev).to(torch.bfloat16)
         w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
         nout = N // 2 if epi == L.EPI_SWIGLU else N
@@ -62,8 +82,9 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 times[t].append(e0.elapsed_time(e1) / args.iters)
+        fill = timeit_fill(out, args)
         fl = 2.0 * M * N * K
-        line = f"{name} N={N:5d} K={K:4d}:"
+        line = f"{name} N={N:5d} K={K:4d} [fill {fill * 1e3:6.1f}us {out.numel() * 2 / fill / 1e9:5.2f}TB/s]:"
         for t in tiles:
             ms = sorted(times[t])[len(times[t]) // 2]
             line += f"  t{t} {ms * 1e3:7.1f}us {fl / ms / 1e9:6.0f}TF{'' if same[t] else ' MISMATCH'}"
