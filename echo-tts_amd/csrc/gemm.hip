@@ -38,18 +38,29 @@ __device__ __forceinline__ float epi_pointwise(float v, const Epi& ep) {
   return v;
 }
 
+// Epilogue kinds, resolved on the host (ek_of) so the hot GEMMs get straight-line code:
+// EK_GENERIC handles every Epi combination with runtime flags; the specialised kinds cover the
+// decoder's three hot shapes (QKVG store, W13 SwiGLU, Wo/W2 gated residual) without bias/act/div.
+enum { EK_GENERIC = 0, EK_STORE = 1, EK_SWIGLU = 2, EK_RESID = 3 };
+
+// SiLU for the SwiGLU epilogue: hardware exp2 + reciprocal (≈2 ulp fp32 before the bf16 rounding
+// that follows; the reference's bf16 F.silu rounds the same value, model.py:118-122).
+__device__ __forceinline__ float silu_hw(float a) {
+  return a * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(a * -1.44269504088896341f));
+}
+
 // Epilogue shared by the bf16 kernels (must follow a barrier after the last LDS read):
 // stage 1 registers -> per-wave swizzled LDS tile (bf16-rounded, bias/act/div or SwiGLU);
 // stage 2 16-B row chunks -> residual/gate tail -> coalesced stores.
-template <int TM, int TN, int FM, int FN>
+template <int TM, int TN, int FM, int FN, int EK>
 __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds, int wid, int wm, int wn, int lane,
                                               int m0, int n0, int M, int N, int z, void* __restrict__ Cv,
                                               int64_t ldc, int64_t sC, const Epi& ep) {
-  const bool swiglu = ep.epi == ECHO_EPI_SWIGLU;
+  const bool swiglu = EK == EK_GENERIC ? ep.epi == ECHO_EPI_SWIGLU : EK == EK_SWIGLU;
   const int TNo = swiglu ? TN / 2 : TN;  // staged columns per wave row
   const int CH = TNo / 8;                // 16-B chunks per staged row
   bf16_t* stg = lds + wid * (TM * TN);
-  const bf16_t* biasp = ep.bias ? (const bf16_t*)ep.bias + z * ep.stride_bias : nullptr;
+  const bf16_t* biasp = (EK == EK_GENERIC && ep.bias) ? (const bf16_t*)ep.bias + z * ep.stride_bias : nullptr;
   const int cq = 4 * (lane >> 4);
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
@@ -61,7 +72,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float a = rbf(acc[i][2 * jj][r]), b = rbf(acc[i][2 * jj + 1][r]);
-          u[r] = rbf(rbf(silu_f(a)) * b);
+          u[r] = rbf(silu_hw(a)) * b;
         }
         const int c0 = jj * 16 + cq;
         const int ph = ((c0 >> 3) ^ (ml & (CH - 1))) * 8 + (c0 & 7);
@@ -75,8 +86,11 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float x = acc[i][j][r];
-          if (biasp) x += bf2f(biasp[min(n0 + wn * TN + nl + r, N - 1)]);
-          v[r] = epi_pointwise(x, ep);
+          if (EK == EK_GENERIC) {
+            if (biasp) x += bf2f(biasp[min(n0 + wn * TN + nl + r, N - 1)]);
+            x = epi_pointwise(x, ep);
+          }
+          v[r] = x;  // pack2bf rounds (RNE) exactly once
         }
         const int ph = ((nl >> 3) ^ (ml & (CH - 1))) * 8 + (nl & 7);
         *(uint2*)(stg + ml * TNo + ph) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
@@ -89,6 +103,53 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
   // ---- epilogue, stage 2: row chunks -> fused row-wise tail -> 16-B stores
   const int Nout = swiglu ? N / 2 : N;
   const int nbase = (swiglu ? n0 / 2 : n0) + wn * TNo;
+  if constexpr (EK != EK_GENERIC) {
+    // all of this lane's chunks are read (LDS, and the residual rows) before any store, so
+    // the long-latency loads overlap; in-place residual (aux == C) is safe because every
+    // element is read and written by the same lane.
+    constexpr int CHc = (EK == EK_SWIGLU ? TN / 2 : TN) / 8, RPIc = 64 / CHc, NIT = TM / RPIc;
+    const int c = lane % CHc;
+    const int n = nbase + c * 8;
+    u32x4 d[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int row = it * RPIc + lane / CHc;
+      d[it] = *(const u32x4*)(stg + row * CHc * 8 + ((c ^ (row & (CHc - 1))) * 8));
+    }
+    if (n >= Nout) return;
+    if constexpr (EK == EK_RESID) {
+      float g[8];
+      if (ep.gate) load8((const bf16_t*)ep.gate + z * ep.stride_gate + n, g);
+      const bf16_t* auxp = (const bf16_t*)ep.aux + z * ep.stride_aux + n;
+      u32x4 x[NIT];
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int m = min(m0 + wm * TM + it * RPIc + lane / CHc, M - 1);
+        x[it] = *(const u32x4*)(auxp + (int64_t)m * ep.ld_aux);
+      }
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        float v[8], xf[8];
+        const bf16_t* dv = (const bf16_t*)&d[it];
+        const bf16_t* xv = (const bf16_t*)&x[it];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = bf2f(dv[e]);
+          xf[e] = bf2f(xv[e]);
+          if (ep.gate) v[e] = rbf(g[e] * v[e]);
+          v[e] = xf[e] + v[e];
+        }
+        d[it] = u32x4{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+      }
+    }
+    bf16_t* Cp = (bf16_t*)Cv + z * sC + n;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int m = m0 + wm * TM + it * RPIc + lane / CHc;
+      if (m < M) *(u32x4*)(Cp + (int64_t)m * ldc) = d[it];
+    }
+    return;
+  }
   const int RPI = 64 / CH;
   const int c = lane % CH;
   for (int it = 0; it < TM / RPI; ++it) {
@@ -118,7 +179,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int EK>
 __global__ void __launch_bounds__(64 * WM * WN)
 gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
                  const bf16_t* __restrict__ W, int64_t ldw, int64_t sW,
@@ -216,7 +277,7 @@ gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
     __syncthreads();
   }
 
-  gemm_epilogue<TM, TN, FM, FN>(acc, lds, wid, wm, wn, lane, m0, n0, M, N, z, Cv, ldc, sC, ep);
+  gemm_epilogue<TM, TN, FM, FN, EK>(acc, lds, wid, wm, wn, lane, m0, n0, M, N, z, Cv, ldc, sC, ep);
 }
 
 // ----------------------------------------------------------------------------- 256x256 ping-pong
@@ -250,7 +311,8 @@ __device__ __forceinline__ int chunk_row(int c, int g) {
   return (g >> 2) * 64 + (c == 2 ? 32 : 0) + (g & 3) * 8;
 }
 
-template <int ABL>  // ablation (timing experiments only): 1 = no in-loop DMA, 2 = no fragment reads, 3 = both
+template <int ABL, int EK>  // ABL: timing ablations only (1 no in-loop DMA, 2 no fragment reads, 4 no
+                            // epilogue stores, 8 no epilogue); EK: epilogue kind
 __global__ void __launch_bounds__(512)
 gemm_bf16_pp_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
                     const bf16_t* __restrict__ W, int64_t ldw, int64_t sW,
@@ -309,10 +371,10 @@ gemm_bf16_pp_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   };
 
   const int nk = K / BK;
-  // prologue: K-tile 0 whole
+  // prologue: K-tile 0 whole; phase 0 reads only chunks 0-1, chunks 2-3 retire at its vm_wait(2)
 #pragma unroll
   for (int c = 0; c < 4; ++c) dma(c, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   pp_barrier();
   if (wm == 1) pp_barrier();  // waves 4-7 run one barrier (half a phase) behind
 
@@ -378,7 +440,7 @@ gemm_bf16_pp_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   }
   Epi e2 = ep;
   if (ABL & 4) e2.epi = 99;  // timing ablation: stage 2 loads/stores skipped
-  gemm_epilogue<TM, TN, FM, FN>(acc, lds, wid, wm, wn, lane, m0, n0, M, N, z, Cv, ldc, sC, e2);
+  gemm_epilogue<TM, TN, FM, FN, EK>(acc, lds, wid, wm, wn, lane, m0, n0, M, N, z, Cv, ldc, sC, e2);
 }
 
 // ----------------------------------------------------------------------------- fp32 (parity mode)
@@ -473,25 +535,57 @@ int pick_tile(int M, int N, int K, int batch) {
   return best;
 }
 
-template <int BM, int BN, int WM, int WN>
-int launch_bf16(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
+template <int BM, int BN, int WM, int WN, int EK>
+int launch_bf16_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;
   dim3 grid(tm * tn, a->batch);
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN>), grid, dim3(64 * WM * WN), 0, s,
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, EK>), grid, dim3(64 * WM * WN), 0, s,
                      (const bf16_t*)a->A, a->lda, a->stride_a, (const bf16_t*)a->W, a->ldw, a->stride_w,
                      a->C, a->ldc, a->stride_c, a->M, a->N, a->K, tm, tn, ep);
   ECHO_LAUNCH_CHECK();
   return 0;
 }
 
-template <int ABL>
-int launch_pp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
+template <int ABL, int EK>
+int launch_pp_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   const int tm = (a->M + 255) / 256, tn = (a->N + 255) / 256;
-  hipLaunchKernelGGL(gemm_bf16_pp_kernel<ABL>, dim3(tm * tn, a->batch), dim3(512), 0, s, (const bf16_t*)a->A,
+  hipLaunchKernelGGL((gemm_bf16_pp_kernel<ABL, EK>), dim3(tm * tn, a->batch), dim3(512), 0, s, (const bf16_t*)a->A,
                      a->lda, a->stride_a, (const bf16_t*)a->W, a->ldw, a->stride_w, a->C, a->ldc, a->stride_c,
                      a->M, a->N, a->K, tm, tn, ep);
   ECHO_LAUNCH_CHECK();
   return 0;
+}
+
+// epilogue kind of a call: the specialised kinds need no bias, no activation and no divisor
+int ek_of(const EchoGemmArgs* a) {
+  if (a->bias || a->act != ECHO_ACT_NONE || a->out_div != 0.0f) return EK_GENERIC;
+  switch (a->epilogue) {
+    case ECHO_EPI_STORE: return EK_STORE;
+    case ECHO_EPI_SWIGLU: return EK_SWIGLU;
+    case ECHO_EPI_RESID: return EK_RESID;
+    default: return EK_GENERIC;
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_bf16(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
+  switch (ek_of(a)) {
+    case EK_STORE: return launch_bf16_ek<BM, BN, WM, WN, EK_STORE>(a, ep, s);
+    case EK_SWIGLU: return launch_bf16_ek<BM, BN, WM, WN, EK_SWIGLU>(a, ep, s);
+    case EK_RESID: return launch_bf16_ek<BM, BN, WM, WN, EK_RESID>(a, ep, s);
+    default: return launch_bf16_ek<BM, BN, WM, WN, EK_GENERIC>(a, ep, s);
+  }
+}
+
+template <int ABL>
+int launch_pp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
+  if (ABL != 0) return launch_pp_ek<ABL, EK_GENERIC>(a, ep, s);
+  switch (ek_of(a)) {
+    case EK_STORE: return launch_pp_ek<0, EK_STORE>(a, ep, s);
+    case EK_SWIGLU: return launch_pp_ek<0, EK_SWIGLU>(a, ep, s);
+    case EK_RESID: return launch_pp_ek<0, EK_RESID>(a, ep, s);
+    default: return launch_pp_ek<0, EK_GENERIC>(a, ep, s);
+  }
 }
 
 }  // namespace
