@@ -443,6 +443,141 @@ gemm_bf16_pp_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   gemm_epilogue<TM, TN, FM, FN, EK>(acc, lds, wid, wm, wn, lane, m0, n0, M, N, z, Cv, ldc, sC, e2);
 }
 
+// ----------------------------------------------------------------------------- 2-phase ping-pong
+// Same tile, LDS image, chunking and epilogue as gemm_bf16_pp_kernel, but a K-tile is 2 phases of
+// 32 MFMAs (half the barriers per MFMA): phase 0 = A rows qm=0 x all 64 B columns of the wave,
+// phase 1 = A rows qm=1 x the same B fragments (held in registers, never re-read).
+//   * every L segment retires its fragment reads (lgkmcnt(0)) BEFORE its barrier, so a chunk's
+//     region is free as soon as the reader's next barrier has passed;
+//   * DMA runs 1.5 K-tiles ahead: chunks 0-2 (A qm0 rows + all B) of tile kt+2 are issued in
+//     phase 1 of tile kt (their region of buffer kt&1 was last read in phase 0), chunk 3 (A qm1)
+//     of tile kt+1 in phase 0 of tile kt (region last read in phase 1 of tile kt-1);
+//   * each chunk is waited for 4 segments (2 phases) after issue: steady state vmcnt(8).
+template <int N> __device__ __forceinline__ void vm_wait_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int EK>
+__global__ void __launch_bounds__(512)
+gemm_bf16_pp2_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
+                     const bf16_t* __restrict__ W, int64_t ldw, int64_t sW,
+                     void* __restrict__ Cv, int64_t ldc, int64_t sC,
+                     int M, int N, int K, int tiles_m, int tiles_n, Epi ep) {
+  constexpr int BM = 256, BN = 256, TM = 128, TN = 64, FM = 8, FN = 4;
+  constexpr int STAGE = (BM + BN) * BK;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int z = blockIdx.y;
+  A += z * sA;
+  W += z * sW;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  constexpr int GM = 8;
+  const int grp = wg / (GM * tiles_n);
+  const int fm = grp * GM;
+  const int gm = min(tiles_m - fm, GM);
+  const int rem = wg - grp * GM * tiles_n;
+  const int tm = fm + rem % gm, tn = rem / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bf16_t* dsrc[4][2];
+  int ddst[4][2];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int rb = chunk_row(c, 2 * wid + h);
+      const int row = rb + (lane >> 3);
+      const int gc = (lane & 7) ^ ((row >> 1) & 7);
+      const bool isA = (c == 0 || c == 3);
+      const int grow = isA ? min(m0 + row, M - 1) : min(n0 + row, N - 1);
+      dsrc[c][h] = (isA ? A + (int64_t)grow * lda : W + (int64_t)grow * ldw) + gc * 8;
+      ddst[c][h] = (isA ? 0 : BM * BK) + rb * BK;
+    }
+  auto dma = [&](int c, int kt) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(dsrc[c][h] + kt * BK),
+          (__attribute__((address_space(3))) void*)(lds + (kt & 1) * STAGE + ddst[c][h]), 16, 0, 0);
+  };
+
+  const int nk = K / BK;
+  // prologue: tile 0 whole, chunks 0-2 of tile 1; wait for chunks 0-2 of tile 0
+#pragma unroll
+  for (int c = 0; c < 4; ++c) dma(c, 0);
+  if (nk > 1) {
+    dma(0, 1); dma(1, 1); dma(2, 1);
+    vm_wait_n<8>();
+  } else {
+    vm_wait_n<2>();
+  }
+  pp_barrier();
+  if (wm == 1) pp_barrier();  // waves 4-7 run one barrier (one segment) behind
+
+  const int frow = lane & 15;
+  const int fsw = frow >> 1;
+  bf16x8 af[4][2], bfr[4][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const bf16_t* As = lds + (kt & 1) * STAGE;
+    const bf16_t* Bs = As + BM * BK;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      // ---- L segment
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          af[i][s] = *(const bf16x8*)(As + (wm * TM + ph * 64 + i * 16 + frow) * BK +
+                                      (((4 * s + (lane >> 4)) ^ fsw) * 8));
+      if (ph == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            bfr[j][s] = *(const bf16x8*)(Bs + (wn * TN + j * 16 + frow) * BK +
+                                         (((4 * s + (lane >> 4)) ^ fsw) * 8));
+        if (n1) dma(3, kt + 1);
+        // retire chunk 3 of tile kt (issued one phase pair ago)
+        if (n1) vm_wait_n<8>(); else vm_wait_n<0>();
+      } else {
+        if (n2) { dma(0, kt + 2); dma(1, kt + 2); dma(2, kt + 2); }
+        // retire chunks 0-2 of tile kt+1
+        if (n2) vm_wait_n<8>(); else if (n1) vm_wait_n<2>(); else vm_wait_n<0>();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      pp_barrier();
+      // ---- C segment
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            acc[ph * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][s], af[i][s], acc[ph * 4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+    }
+  }
+  if (wm == 0) pp_barrier();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  gemm_epilogue<TM, TN, FM, FN, EK>(acc, lds, wid, wm, wn, lane, m0, n0, M, N, z, Cv, ldc, sC, ep);
+}
+
 // ----------------------------------------------------------------------------- fp32 (parity mode)
 constexpr int FT = 64, FK = 16;
 
@@ -513,12 +648,12 @@ gemm_f32_kernel(const float* __restrict__ A, int64_t lda, int64_t sA,
 }
 
 struct TileCfg { int bm, bn, occ; float eff; };
-constexpr TileCfg kTiles[] = {
-    {256, 256, 1, 1.00f},  // 1: 8 waves, 128x64 per wave
-    {256, 128, 1, 0.92f},  // 2: 8 waves, 64x64 per wave
-    {128, 128, 2, 0.80f},  // 3: 4 waves, 64x64 per wave
-    {128, 64, 3, 0.62f},   // 4: 4 waves, 64x32 per wave
-    {64, 64, 4, 0.40f},    // 5: 4 waves, 32x32 per wave
+constexpr TileCfg kTiles[] = {  // eff: per-tile throughput relative to the 2-phase ping-pong 256x256
+    {256, 256, 1, 1.00f},  // 1: 8 waves, 128x64 per wave (runs gemm_bf16_pp2_kernel)
+    {256, 128, 1, 0.68f},  // 2: 8 waves, 64x64 per wave
+    {128, 128, 2, 0.64f},  // 3: 4 waves, 64x64 per wave
+    {128, 64, 3, 0.50f},   // 4: 4 waves, 64x32 per wave
+    {64, 64, 4, 0.32f},    // 5: 4 waves, 32x32 per wave
 };
 
 int pick_tile(int M, int N, int K, int batch) {
@@ -556,6 +691,16 @@ int launch_pp_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   return 0;
 }
 
+template <int EK>
+int launch_pp2_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
+  const int tm = (a->M + 255) / 256, tn = (a->N + 255) / 256;
+  hipLaunchKernelGGL((gemm_bf16_pp2_kernel<EK>), dim3(tm * tn, a->batch), dim3(512), 0, s, (const bf16_t*)a->A,
+                     a->lda, a->stride_a, (const bf16_t*)a->W, a->ldw, a->stride_w, a->C, a->ldc, a->stride_c,
+                     a->M, a->N, a->K, tm, tn, ep);
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
 // epilogue kind of a call: the specialised kinds need no bias, no activation and no divisor
 int ek_of(const EchoGemmArgs* a) {
   if (a->bias || a->act != ECHO_ACT_NONE || a->out_div != 0.0f) return EK_GENERIC;
@@ -577,6 +722,15 @@ int launch_bf16(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   }
 }
 
+int launch_pp2(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
+  switch (ek_of(a)) {
+    case EK_STORE: return launch_pp2_ek<EK_STORE>(a, ep, s);
+    case EK_SWIGLU: return launch_pp2_ek<EK_SWIGLU>(a, ep, s);
+    case EK_RESID: return launch_pp2_ek<EK_RESID>(a, ep, s);
+    default: return launch_pp2_ek<EK_GENERIC>(a, ep, s);
+  }
+}
+
 template <int ABL>
 int launch_pp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   if (ABL != 0) return launch_pp_ek<ABL, EK_GENERIC>(a, ep, s);
@@ -592,7 +746,7 @@ int launch_pp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 
 extern "C" int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch) {
   const int t = pick_tile(M, N, K, batch);
-  return t == 1 ? 6 : t;
+  return t == 1 ? 13 : t;
 }
 
 extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
@@ -616,7 +770,7 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
   if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C) & 15) return ECHO_EALIGN;
   int t = a->tile > 0 ? a->tile : pick_tile(a->M, a->N, a->K, a->batch);
-  if (a->tile == 0 && t == 1) t = 6;  // 256x256 tiles run the ping-pong schedule (bitwise-identical results)
+  if (a->tile == 0 && t == 1) t = 13;  // 256x256 tiles run the 2-phase ping-pong (bitwise-identical results)
   switch (t) {
     case 1: return launch_bf16<256, 256, 2, 4>(a, ep, s);
     case 2: return launch_bf16<256, 128, 4, 2>(a, ep, s);
@@ -630,6 +784,7 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
     case 10: return launch_pp<4>(a, ep, s);
     case 11: return launch_pp<8>(a, ep, s);
     case 12: return launch_pp<11>(a, ep, s);
+    case 13: return launch_pp2(a, ep, s);
     default: return ECHO_EINVAL;
   }
 }

@@ -5,6 +5,8 @@ every arithmetic op runs in `libecho_hip.so`.
 from __future__ import annotations
 
 import ctypes as C
+import os
+import sys
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -13,6 +15,10 @@ import torch
 from . import _lib as L
 
 Tensor = torch.Tensor
+
+
+# ECHO_DEBUG_SYNC=1: log every GEMM launch and synchronise after it (hang/fault localisation)
+_DEBUG_SYNC = os.environ.get("ECHO_DEBUG_SYNC", "0") == "1"
 
 
 def lib():
@@ -101,7 +107,13 @@ def gemm(a: Tensor, w: Tensor, out: Optional[Tensor] = None, *, bias: Optional[T
                 raise ValueError("gate must be [(B,)N]")
             args.gate, args.stride_gate = gate.data_ptr(), (gate.stride(0) if gate.dim() == 2 else 0)
     args.epilogue, args.act, args.out_div, args.tile = epilogue, act, out_div, tile
+    if _DEBUG_SYNC:
+        print(f"[echo gemm] M={args.M} N={args.N} K={args.K} batch={args.batch} epi={args.epilogue} "
+              f"act={args.act} tile={args.tile} pick={lib().echo_gemm_pick_tile(args.M, args.N, args.K, args.batch)} "
+              f"lda={args.lda} ldw={args.ldw} ldc={args.ldc}", file=sys.stderr, flush=True)
     L.check(lib().echo_gemm(C.byref(args), _stream()), "echo_gemm")
+    if _DEBUG_SYNC:
+        torch.cuda.synchronize()
     return out
 
 

@@ -49,7 +49,7 @@ def _seed():
     torch.manual_seed(0)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 13])
 @pytest.mark.parametrize("M,N,K", [(640, 2048, 2048), (200, 208, 320), (1, 80, 128), (1000, 4096, 576)])
 def test_gemm_store_bias(tile, M, N, K):
     a = torch.randn(M, K, device=DEV).to(BF)
@@ -59,7 +59,7 @@ def test_gemm_store_bias(tile, M, N, K):
     close_bf16(out, rb(ref_linear(a, w, b)))
 
 
-@pytest.mark.parametrize("tile", [1, 3, 5, 6])
+@pytest.mark.parametrize("tile", [1, 3, 5, 6, 13])
 def test_gemm_swiglu(tile):
     M, F, K = 333, 704, 256
     a = torch.randn(M, K, device=DEV).to(BF)
@@ -72,7 +72,7 @@ def test_gemm_swiglu(tile):
     close_bf16(out, ref)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 4, 6])
+@pytest.mark.parametrize("tile", [1, 2, 4, 6, 13])
 @pytest.mark.parametrize("with_gate", [True, False])
 def test_gemm_resid(tile, with_gate):
     M, N, K = 517, 512, 1024
@@ -116,12 +116,14 @@ def test_gemm_act_div_f32out_batched():
         close_bf16(raw[i, :, 1], ref)
 
 
-@pytest.mark.parametrize("M,N,K", [(1000, 4096, 576), (256, 256, 64), (300, 512, 2048)])
+@pytest.mark.parametrize("M,N,K", [(1000, 4096, 576), (256, 256, 64), (512, 768, 128), (300, 512, 2048)])
 def test_gemm_pingpong_bitwise(M, N, K):
     """The ping-pong schedule accumulates in the same K order as the baseline kernel."""
     a = torch.randn(M, K, device=DEV).to(BF)
     w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
-    assert torch.equal(ops.gemm(a, w, tile=1), ops.gemm(a, w, tile=6))
+    ref = ops.gemm(a, w, tile=1)
+    assert torch.equal(ref, ops.gemm(a, w, tile=6))
+    assert torch.equal(ref, ops.gemm(a, w, tile=13))
 
 
 def test_gemm_f32():

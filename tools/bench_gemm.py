@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--tiles", default="1,6")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--torch", action="store_true", help="also time torch.nn.functional.linear (hipBLASLt)")
     ap.add_argument("--shapes", default=None, help="M,N,K[,epi];... overrides the production list")
     args = ap.parse_args()
     shapes = SHAPES
@@ -83,11 +84,25 @@ def main():
                 torch.cuda.synchronize()
                 times[t].append(e0.elapsed_time(e1) / args.iters)
         fill = timeit_fill(out, args)
+        tl = None
+        if args.torch:
+            ts = []
+            for _ in range(args.rounds):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.iters):
+                    torch.nn.functional.linear(a, w)
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1) / args.iters)
+            tl = sorted(ts)[len(ts) // 2]
         fl = 2.0 * M * N * K
         line = f"{name} N={N:5d} K={K:4d} [fill {fill * 1e3:6.1f}us {out.numel() * 2 / fill / 1e9:5.2f}TB/s]:"
         for t in tiles:
             ms = sorted(times[t])[len(times[t]) // 2]
             line += f"  t{t} {ms * 1e3:7.1f}us {fl / ms / 1e9:6.0f}TF{'' if same[t] else ' MISMATCH'}"
+        if tl is not None:
+            line += f"  torch {tl * 1e3:7.1f}us {fl / tl / 1e9:6.0f}TF"
         print(line, flush=True)
 
 

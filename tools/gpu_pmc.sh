@@ -7,7 +7,7 @@ TAG=$1; shift
 export TMPDIR=/tmp
 cd /tmp || exit 1
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "gemm_bf16_pp_kernel" --output-format csv \
+  timeout -k 10 ${PMC_TIMEOUT:-600} rocprofv3 --pmc $C --kernel-include-regex "gemm_bf16_pp2_kernel" --output-format csv \
     -d "$R/gpurun_out/pmc_${TAG}_$C" -o pmc -- python "$R/bench.py" --no-graph "$@" \
     > "$R/gpurun_out/pmc_${TAG}_$C.log" 2>&1 || exit $?
 done
