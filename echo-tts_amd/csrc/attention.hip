@@ -42,8 +42,14 @@ __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
-constexpr int QB = 128;  // queries per workgroup
 constexpr int KT = 64;   // keys per tile
+
+// value select (a ?: between two named variables is an lvalue: clang selects their ADDRESSES,
+// which keeps SROA from promoting them and sends them to scratch)
+template <class T>
+__device__ __forceinline__ T sel4(int sg, T a0, T a1, T a2, T a3) {
+  return sg == 3 ? a3 : sg == 2 ? a2 : sg == 1 ? a1 : a0;
+}
 
 struct SegInfo {
   const bf16_t* kb;
@@ -52,15 +58,29 @@ struct SegInfo {
   int kend, causal, first;  // first = index of the segment's first tile in the flat tile list
 };
 
-__global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
-  // [buffer][K | V][64 keys x 128] — one array (keeps hipcc from draining DMA before ds_reads)
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KT * 128];
+// ABL: timing ablations only (tools/bench_attn.py via ECHO_ATTN_ABL; results are wrong):
+// 1 = no in-loop DMA, 2 = no softmax VALU, 4 = no PV (MFMA + V reads), 8 = no QK (MFMA + K reads)
+// NW waves x 32 queries per workgroup (QB = 32 NW). K/V staging: ST = 2 or 3 -> ST-stage LDS ring
+// filled by LDS-DMA (tile t+ST-1 issued at tile t); ST = 0 -> register staging (cdna_hip_programming.md
+// T14): tile t+2 is loaded into VGPRs at the top of tile t and written (swizzled) into the free LDS
+// buffer at the top of tile t+1, so 2 LDS buffers give a 2-tile lookahead.
+template <int ABL, int NW, int ST, int KTT = 64>
+__global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) attn_bf16_kernel(EchoAttnArgs a) {
+  constexpr int QB = 32 * NW;
+  constexpr int DPT = KTT / (4 * NW);  // DMA wave-instructions per wave per K (or V) tile
+  constexpr int NKK = KTT / 32;        // 32-key sub-tiles per tile
+  // [stage][K | V][64 keys x 128] — one array (keeps hipcc from draining DMA before ds_reads)
+  constexpr int NBUF = ST == 0 ? 2 : ST;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[NBUF * 2 * KTT * 128];
 
   const int nqb = (a.n_q + QB - 1) / QB;
   const int L = remap_xcd(blockIdx.x, gridDim.x);
   const int qb = L % nqb;
-  const int head = (L / nqb) % a.heads;
-  const int row = L / (nqb * a.heads);
+  // rows fastest: each XCD's contiguous block range then covers every row type (cond /
+  // uncond-text / uncond-speaker rows have different key counts), and the CFG rows that share
+  // one text/speaker K/V copy land on the same XCD
+  const int row = (L / nqb) % a.rows;
+  const int head = L / (nqb * a.rows);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h2 = lane >> 5, ql = lane & 31;
@@ -79,32 +99,46 @@ __global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
 
   // flat list of 64-key tiles over the (up to 4) segments; per-segment fields are kept in
   // named scalars (no runtime-indexed arrays: those go to scratch)
-  SegInfo s0{}, s1{}, s2{}, s3{};
+  // per-segment fields as named scalars (struct copies / runtime-indexed arrays go to scratch)
+  const bf16_t *kb0 = nullptr, *kb1 = nullptr, *kb2 = nullptr, *kb3 = nullptr;
+  const bf16_t *vb0 = nullptr, *vb1 = nullptr, *vb2 = nullptr, *vb3 = nullptr;
+  int64_t ld0 = 0, ld1 = 0, ld2 = 0, ld3 = 0;
+  int ke0 = 0, ke1 = 0, ke2 = 0, ke3 = 0, ca0 = 0, ca1 = 0, ca2 = 0, ca3 = 0;
+  int fi0 = 0, fi1 = 0, fi2 = 0, fi3 = 0;
   int ntiles = 0;
-  auto init_seg = [&](int sg, SegInfo& d) {
-    d.first = ntiles;
-    if (sg < a.nseg && a.seg[sg].k) {
-      const EchoKVSegment& S = a.seg[sg];
-      const int len = S.len ? S.len[row] : S.capacity;
-      int kend = min(len, S.capacity);
-      if (S.causal) kend = min(kend, q0 + QB);
-      kend = max(kend, 0);
-      const int b = row % S.batch_mod;
-      d.kb = (const bf16_t*)S.k + b * S.ld_batch + head * 128;
-      d.vb = (const bf16_t*)S.v + b * S.ld_batch + head * 128;
-      d.ld = S.ld_tok;
-      d.kend = kend;
-      d.causal = S.causal;
-      ntiles += (kend + KT - 1) / KT;
-    }
-  };
-  init_seg(0, s0);
-  init_seg(1, s1);
-  init_seg(2, s2);
-  init_seg(3, s3);
+#define ECHO_INIT_SEG(SG)                                                                  \
+  fi##SG = ntiles;                                                                         \
+  if (SG < a.nseg && a.seg[SG].k) {                                                        \
+    const int len = a.seg[SG].len ? a.seg[SG].len[row] : a.seg[SG].capacity;              \
+    int kend = min(len, a.seg[SG].capacity);                                               \
+    if (a.seg[SG].causal) kend = min(kend, q0 + QB);                                       \
+    kend = max(kend, 0);                                                                   \
+    const int b = row % a.seg[SG].batch_mod;                                               \
+    kb##SG = (const bf16_t*)a.seg[SG].k + b * a.seg[SG].ld_batch + head * 128;             \
+    vb##SG = (const bf16_t*)a.seg[SG].v + b * a.seg[SG].ld_batch + head * 128;             \
+    ld##SG = a.seg[SG].ld_tok;                                                             \
+    ke##SG = kend;                                                                         \
+    ca##SG = a.seg[SG].causal;                                                             \
+    ntiles += (kend + KTT - 1) / KTT;                                                        \
+  }
+  ECHO_INIT_SEG(0)
+  ECHO_INIT_SEG(1)
+  ECHO_INIT_SEG(2)
+  ECHO_INIT_SEG(3)
+#undef ECHO_INIT_SEG
+  // segment of flat tile ti, each field selected as a scalar
   auto pick = [&](int ti) -> SegInfo {
-    return ti >= s3.first && s3.kend > 0 ? s3 : ti >= s2.first && s2.kend > 0 ? s2
-         : ti >= s1.first && s1.kend > 0 ? s1 : s0;
+    const int sg = ti >= fi3 && ke3 > 0 ? 3 : ti >= fi2 && ke2 > 0 ? 2 : ti >= fi1 && ke1 > 0 ? 1 : 0;
+#define ECHO_SEL(f) sel4(sg, f##0, f##1, f##2, f##3)
+    SegInfo d;
+    d.kb = ECHO_SEL(kb);
+    d.vb = ECHO_SEL(vb);
+    d.ld = ECHO_SEL(ld);
+    d.kend = ECHO_SEL(ke);
+    d.causal = ECHO_SEL(ca);
+    d.first = ECHO_SEL(fi);
+#undef ECHO_SEL
+    return d;
   };
 
   // DMA of tile ti into buffer `buf`: 64 rows x 256 B for K and V = 32 wave-instructions
@@ -112,15 +146,15 @@ __global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
   const int dr = lane >> 4, dp = lane & 15;
   auto dma_tile = [&](int ti, int buf) {
     const SegInfo d = pick(ti);
-    const int t0 = (ti - d.first) * KT;
+    const int t0 = (ti - d.first) * KTT;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = (i * 4 + w) * 4 + dr;  // tile row 0..63 written by this lane
+    for (int i = 0; i < DPT; ++i) {
+      const int r = (i * NW + w) * 4 + dr;  // tile row 0..63 written by this lane
       const int64_t tok = min(t0 + r, d.kend - 1);
       const int c = dp ^ swz(r);
-      const int dst = ((i * 4 + w) * 4) * 128;
-      const uint32_t kdst = __builtin_amdgcn_readfirstlane(lds_addr_of(lds + (buf * 2) * KT * 128 + dst));
-      const uint32_t vdst = __builtin_amdgcn_readfirstlane(lds_addr_of(lds + (buf * 2 + 1) * KT * 128 + dst));
+      const int dst = ((i * NW + w) * 4) * 128;
+      const uint32_t kdst = __builtin_amdgcn_readfirstlane(lds_addr_of(lds + (buf * 2) * KTT * 128 + dst));
+      const uint32_t vdst = __builtin_amdgcn_readfirstlane(lds_addr_of(lds + (buf * 2 + 1) * KTT * 128 + dst));
       glds16(d.kb + tok * d.ld + c * 8, kdst);
       glds16(d.vb + tok * d.ld + c * 8, vdst);
     }
@@ -135,27 +169,72 @@ __global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
   const float sl2 = a.scale * 1.4426950408889634f;
   const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
 
-  if (ntiles > 0) dma_tile(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // register staging: thread t moves 16-B chunks c = t + i*64*NW (row c>>4, chunk c&15) of K and V
+  u32x4 kreg[DPT], vreg[DPT];
+  auto load_tile = [&](int ti) {
+    const SegInfo d = pick(ti);
+    const int t0 = (ti - d.first) * KTT;
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int c = tid + i * 64 * NW;
+      const int64_t tok = min(t0 + (c >> 4), d.kend - 1);
+      kreg[i] = *(const u32x4*)(d.kb + tok * d.ld + (c & 15) * 8);
+      vreg[i] = *(const u32x4*)(d.vb + tok * d.ld + (c & 15) * 8);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int c = tid + i * 64 * NW;
+      const int r = c >> 4;
+      const int off = r * 128 + (((c & 15) ^ swz(r)) * 8);
+      *(u32x4*)(lds + (buf * 2) * KTT * 128 + off) = kreg[i];
+      *(u32x4*)(lds + (buf * 2 + 1) * KTT * 128 + off) = vreg[i];
+    }
+  };
+
+  if constexpr (ST == 0) {
+    if (ntiles > 0) { load_tile(0); store_tile(0); }
+    if (ntiles > 1) load_tile(1);
+  } else {
+    // prologue: tiles 0 .. ST-2 in flight, wait for tile 0
+#pragma unroll
+    for (int p = 0; p < ST - 1; ++p)
+      if (p < ntiles) dma_tile(p, p);
+    if (ST == 3 && ntiles > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
 
+  int cur = 0;
+  if (ABL & 64) ntiles = 0;
   for (int ti = 0; ti < ntiles; ++ti) {
-    const int cur = ti & 1;
-    if (ti + 1 < ntiles) dma_tile(ti + 1, cur ^ 1);  // lands while this tile computes
-    const bf16_t* Ks = lds + (cur * 2) * KT * 128;
-    const bf16_t* Vs = Ks + KT * 128;
+    if constexpr (ST == 0) {
+      // buffer cur^1 held tile ti-1: every wave passed the barrier after reading it
+      if (ti + 1 < ntiles && !(ABL & 1)) store_tile(cur ^ 1);
+      if (ti + 2 < ntiles && !(ABL & 1)) load_tile(ti + 2);
+    } else {
+      // tile ti+ST-1 into the stage tile ti-1 used (all waves passed the barrier after reading it)
+      if (ti + ST - 1 < ntiles && !(ABL & 1)) dma_tile(ti + ST - 1, cur == 0 ? ST - 1 : cur - 1);
+    }
+    const bf16_t* Ks = lds + (cur * 2) * KTT * 128;
+    const bf16_t* Vs = Ks + KTT * 128;
     const SegInfo d = pick(ti);
-    const int t0 = (ti - d.first) * KT;
+    const int t0 = (ti - d.first) * KTT;
     const int kend = d.kend;
-    const bool full = (t0 + KT <= kend) && !d.causal;
+    const bool full = (t0 + KTT <= kend) && !d.causal;
 
     // ---- S^T = K . Q^T for two 32-key sub-tiles
-    f32x16 st[2];
+    f32x16 st[NKK];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < NKK; ++kk) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) st[kk][r] = 0.f;
       const int kr_ = kk * 32 + ql;
+      if (ABL & 8) {
+        for (int r = 0; r < 16; ++r) st[kk][r] = bf2f(qf[r & 7][r >> 3]);
+        continue;
+      }
 #pragma unroll
       for (int ds = 0; ds < 8; ++ds) {
         const int c = 2 * ds + h2;
@@ -167,9 +246,10 @@ __global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
     // The running max is kept on RAW scores (scale > 0 preserves the argmax); one FMA per score
     // forms the exp2 argument s*c - m*c; raw v_exp_f32 (results < 2^-126 flush to 0).
     float mx = -INFINITY;
+    if (!(ABL & 2)) {
     if (!full) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < NKK; ++kk)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = t0 + kk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
@@ -178,7 +258,7 @@ __global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
         }
     }
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int kk = 0; kk < NKK; ++kk)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) mx = fmaxf(mx, fmaxf(st[kk][r], st[kk][r + 1]));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
@@ -186,7 +266,7 @@ __global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
     const float msc = m_new == -INFINITY ? 0.f : -m_new * sl2;
     float psum = 0.f;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int kk = 0; kk < NKK; ++kk)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(st[kk][r], sl2, msc));
@@ -203,35 +283,340 @@ __global__ void __launch_bounds__(256, 2) attn_bf16_kernel(EchoAttnArgs a) {
     }
     l_run += psum;
     m_run = m_new;
+    }
 
     // ---- O^T += V^T . P  (P from the accumulators, V^T by transposed LDS reads)
+#pragma unroll
+    for (int kk = 0; kk < ((ABL & 4) ? 0 : NKK); ++kk)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 pf;
+        if (ABL & 32) {
+          pf = qf[kk * 2 + s2];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pf[j] = (__bf16)st[kk][8 * s2 + j];
+        }
+        const int key0 = kk * 32 + 16 * s2 + 4 * h2;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int ch = 4 * dt + 2 * (g & 1) + (p4 >> 1);
+          const int r0 = key0 + q4, r1 = key0 + 8 + q4;
+          typedef __attribute__((ext_vector_type(8))) short s16x8;
+          s16x8 v8;
+          if (ABL & 16) {
+            v8 = __builtin_bit_cast(s16x8, qf[4 + dt]);
+          } else {
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(Vs + r0 * 128 + ((ch ^ swz(r0)) * 8) + (p4 & 1) * 4));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(Vs + r1 * 128 + ((ch ^ swz(r1)) * 8) + (p4 & 1) * 4));
+          v8 = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          }
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf, o[dt], 0, 0, 0);
+        }
+      }
+    if constexpr (ST == 0) {
+      __syncthreads();  // tile ti+1 was written at the top of this tile
+      cur ^= 1;
+    } else {
+      // tile ti+1 landed (this wave's share; later tiles may stay in flight) ... and everyone's
+      if (ST == 3 && ti + 2 < ntiles && !(ABL & 1)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      cur = cur == ST - 1 ? 0 : cur + 1;
+    }
+  }
+
+  // ---- epilogue: normalise, round, gate, store (4 consecutive d per register group)
+  const float lt = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.0f / lt;
+  if (qi >= a.n_q) return;
+  bf16_t* op = (bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qi * a.o_ld_tok + head * 128;
+  const bf16_t* gp = a.gate ? (const bf16_t*)a.gate + row * a.g_ld_batch + (int64_t)qi * a.g_ld_tok + head * 128
+                            : nullptr;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      const int d = dt * 32 + 8 * rg + 4 * h2;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = rbf(o[dt][4 * rg + e] * inv);
+      if (gp) {
+        const uint2 gg = *(const uint2*)(gp + d);
+        const float gv[4] = {bf2f(gg.x & 0xffffu), bf2f(gg.x >> 16), bf2f(gg.y & 0xffffu), bf2f(gg.y >> 16)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = rbf(v[e] * rbf(sigmoid_f(gv[e])));
+      }
+      *(uint2*)(op + d) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+    }
+}
+
+// ----------------------------------------------------------------------------- software-pipelined
+// Same tile math, LDS image and numerics as attn_bf16_kernel<0,4,2>, scheduled so that every wave
+// overlaps its own MFMA and VALU work (cdna_hip_programming.md T15):
+//   phase A of iteration t: S(t+1) = K(t+1).Q^T (16 MFMA)  ||  softmax finish of tile t
+//                           (exp2, row sums, bf16 pack of P(t))
+//   phase B of iteration t: O^T += V(t)^T.P(t) (16 MFMA)   ||  row max of S(t+1)
+// K and V have separate double buffers: K(t+2) and V(t+1) are issued at the top of iteration t
+// (their slots held K(t) and V(t-1), both consumed in iteration t-1); one barrier per iteration.
+// sched_group_barrier pins the MFMA / LDS-read / VALU interleave (T19).
+constexpr int SG_MFMA = 0x8, SG_VALU = 0x2, SG_DSR = 0x100, SG_TRANS = 0x400;
+
+template <int ABL>
+__global__ void __launch_bounds__(256, 1) attn_pipe_kernel(EchoAttnArgs a) {
+  constexpr int NW = 4, QB = 128, DPT = 4;
+  constexpr int NS = 3;  // ring slots per K and per V
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * NS * KT * 128];  // K slots | V slots
+
+  const int nqb = (a.n_q + QB - 1) / QB;
+  const int L = remap_xcd(blockIdx.x, gridDim.x);
+  const int qb = L % nqb;
+  // rows fastest: each XCD's contiguous block range then covers every row type (cond /
+  // uncond-text / uncond-speaker rows have different key counts), and the CFG rows that share
+  // one text/speaker K/V copy land on the same XCD
+  const int row = (L / nqb) % a.rows;
+  const int head = L / (nqb * a.rows);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h2 = lane >> 5, ql = lane & 31;
+  const int q0 = qb * QB;
+  const int qi = q0 + w * 32 + ql;
+  const int qc = min(qi, a.n_q - 1);
+
+  const bf16_t* qp = (const bf16_t*)a.q + row * a.q_ld_batch + (int64_t)qc * a.q_ld_tok + head * 128;
+  bf16x8 qf[8];
+#pragma unroll
+  for (int ds = 0; ds < 8; ++ds) qf[ds] = *(const bf16x8*)(qp + 16 * ds + 8 * h2);
+#pragma unroll
+  for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));
+
+  const bf16_t *kb0 = nullptr, *kb1 = nullptr, *kb2 = nullptr, *kb3 = nullptr;
+  const bf16_t *vb0 = nullptr, *vb1 = nullptr, *vb2 = nullptr, *vb3 = nullptr;
+  int64_t ld0 = 0, ld1 = 0, ld2 = 0, ld3 = 0;
+  int ke0 = 0, ke1 = 0, ke2 = 0, ke3 = 0, ca0 = 0, ca1 = 0, ca2 = 0, ca3 = 0;
+  int fi0 = 0, fi1 = 0, fi2 = 0, fi3 = 0;
+  int ntiles = 0;
+#define ECHO_INIT_SEG(SG)                                                                  \
+  fi##SG = ntiles;                                                                         \
+  if (SG < a.nseg && a.seg[SG].k) {                                                        \
+    const int len = a.seg[SG].len ? a.seg[SG].len[row] : a.seg[SG].capacity;              \
+    int kend = min(len, a.seg[SG].capacity);                                               \
+    if (a.seg[SG].causal) kend = min(kend, q0 + QB);                                       \
+    kend = max(kend, 0);                                                                   \
+    const int b = row % a.seg[SG].batch_mod;                                               \
+    kb##SG = (const bf16_t*)a.seg[SG].k + b * a.seg[SG].ld_batch + head * 128;             \
+    vb##SG = (const bf16_t*)a.seg[SG].v + b * a.seg[SG].ld_batch + head * 128;             \
+    ld##SG = a.seg[SG].ld_tok;                                                             \
+    ke##SG = kend;                                                                         \
+    ca##SG = a.seg[SG].causal;                                                             \
+    ntiles += (kend + KT - 1) / KT;                                                        \
+  }
+  ECHO_INIT_SEG(0)
+  ECHO_INIT_SEG(1)
+  ECHO_INIT_SEG(2)
+  ECHO_INIT_SEG(3)
+#undef ECHO_INIT_SEG
+  auto pick = [&](int ti) __attribute__((always_inline)) -> SegInfo {
+    const int sg = ti >= fi3 && ke3 > 0 ? 3 : ti >= fi2 && ke2 > 0 ? 2 : ti >= fi1 && ke1 > 0 ? 1 : 0;
+#define ECHO_SEL(f) sel4(sg, f##0, f##1, f##2, f##3)
+    SegInfo d;
+    d.kb = ECHO_SEL(kb);
+    d.vb = ECHO_SEL(vb);
+    d.ld = ECHO_SEL(ld);
+    d.kend = ECHO_SEL(ke);
+    d.causal = ECHO_SEL(ca);
+    d.first = ECHO_SEL(fi);
+#undef ECHO_SEL
+    return d;
+  };
+
+  // K (part 0) or V (part 1) of tile ti into its slot: 64 rows x 256 B = 16 wave-instructions
+  const int dr = lane >> 4, dp = lane & 15;
+  auto dma_part = [&](int ti, int part) __attribute__((always_inline)) {
+    const SegInfo d = pick(ti);
+    const int t0 = (ti - d.first) * KT;
+    const bf16_t* base = part ? d.vb : d.kb;
+    const bf16_t* slot = lds + (part * NS + ti % NS) * KT * 128;
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int r = (i * NW + w) * 4 + dr;
+      const int64_t tok = min(t0 + r, d.kend - 1);
+      const int c = dp ^ swz(r);
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr_of(slot + ((i * NW + w) * 4) * 128));
+      glds16(base + tok * d.ld + c * 8, dst);
+    }
+  };
+  // -inf for keys past the segment's valid length (and above the diagonal when causal)
+  auto mask_tile = [&](int ti, f32x16 (&st)[2]) __attribute__((always_inline)) {
+    const SegInfo d = pick(ti);
+    const int t0 = (ti - d.first) * KT;
+    if (t0 + KT <= d.kend && !d.causal) return;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = t0 + kk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
+        const bool ok = key < d.kend && (!d.causal || key <= qi);
+        st[kk][r] = ok ? st[kk][r] : -INFINITY;
+      }
+  };
+  auto qk_tile = [&](const bf16_t* Ks, f32x16 (&st)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st[kk][r] = 0.f;
+      const int kr = kk * 32 + ql;
+#pragma unroll
+      for (int ds = 0; ds < 8; ++ds) {
+        const bf16x8 kf = *(const bf16x8*)(Ks + kr * 128 + (((2 * ds + h2) ^ swz(kr)) * 8));
+        st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], st[kk], 0, 0, 0);
+      }
+    }
+  };
+  auto row_max = [&](const f32x16 (&st)[2]) __attribute__((always_inline)) -> float {
+    float m0 = -INFINITY, m1 = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      m0 = fmaxf(m0, fmaxf(st[0][r], st[0][r + 1]));
+      m1 = fmaxf(m1, fmaxf(st[1][r], st[1][r + 1]));
+    }
+    // permlane32_swap(x, x): r[0] = {x.lo, x.lo}, r[1] = {x.hi, x.hi} -> both halves in every lane
+    const float m = fmaxf(m0, m1);
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+    return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+  };
+
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+  const float sl2 = a.scale * 1.4426950408889634f;
+  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+
+  // iteration t: sc = raw scores of tile t (masked), mxc = their row max; produces sn / mxn for t+1
+  auto iter = [&](int t, f32x16 (&sc)[2], float mxc, f32x16 (&sn)[2], float& mxn) __attribute__((always_inline)) {
+    const bool has_next = t + 1 < ntiles;
+    // K(t+3) into the slot of K(t) (consumed by QK(t) in iteration t-1), V(t+2) into the slot of
+    // V(t-1) (consumed by PV(t-1)); both waited for two iterations later
+    const int nk = t + 3 < ntiles, nv = t + 2 < ntiles;
+    if (!(ABL & 1)) {
+      if (nk) dma_part(t + 3, 0);
+      if (nv) dma_part(t + 2, 1);
+    }
+    const bf16_t* Kn = lds + ((t + 1) % NS) * KT * 128;
+    const bf16_t* Vc = lds + (NS + t % NS) * KT * 128;
+    const float m_new = fmaxf(m_run, mxc);
+    const float msc = m_new == -INFINITY ? 0.f : -m_new * sl2;
+    if (__any(m_new != m_run)) {  // otherwise alpha == 1 exactly for every lane
+      const float alpha = __builtin_amdgcn_exp2f(__builtin_fmaf(m_run, sl2, msc));
+      l_run *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+    }
+    m_run = m_new;
+
+    // ---- phase A: QK(t+1) || exp / row sum / pack of P(t)
+    bf16x8 pf[4];
+    float ps0 = 0.f, ps1 = 0.f;
+    auto softmax_finish = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kk][8 * s2 + j], sl2, msc));
+            if (j & 1) ps1 += pv; else ps0 += pv;
+            pf[kk * 2 + s2][j] = (__bf16)pv;
+          }
+    };
+    if (has_next) {
+      qk_tile(Kn, sn);
+      softmax_finish();
+      // K fragment reads run 2 MFMAs ahead; per MFMA gap 2 exp + 3 other VALU (MI355X_MICROARCH
+      // 'vector-instruction ISSUE cost': 2x8 + 3x4 + the MFMA's 8 stays near the 32-cycle gap)
+      __builtin_amdgcn_sched_group_barrier(SG_DSR, 2, 0);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+        if (k < 14) __builtin_amdgcn_sched_group_barrier(SG_DSR, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_TRANS, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_VALU, 3, 0);
+      }
+    } else {
+      softmax_finish();
+    }
+    l_run += ps0 + ps1;
+
+    // ---- phase B: PV(t) || row max of S(t+1)
+    if (has_next) mask_tile(t + 1, sn);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 pf;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pf[j] = (__bf16)st[kk][8 * s2 + j];
         const int key0 = kk * 32 + 16 * s2 + 4 * h2;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
           const int ch = 4 * dt + 2 * (g & 1) + (p4 >> 1);
           const int r0 = key0 + q4, r1 = key0 + 8 + q4;
           const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(Vs + r0 * 128 + ((ch ^ swz(r0)) * 8) + (p4 & 1) * 4));
+              (__attribute__((address_space(3))) s16x4*)(Vc + r0 * 128 + ((ch ^ swz(r0)) * 8) + (p4 & 1) * 4));
           const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(Vs + r1 * 128 + ((ch ^ swz(r1)) * 8) + (p4 & 1) * 4));
+              (__attribute__((address_space(3))) s16x4*)(Vc + r1 * 128 + ((ch ^ swz(r1)) * 8) + (p4 & 1) * 4));
           typedef __attribute__((ext_vector_type(8))) short s16x8;
           const s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf, o[dt], 0, 0, 0);
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf[kk * 2 + s2], o[dt],
+                                                           0, 0, 0);
         }
       }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next tile landed (this wave's share)
-    __syncthreads();                                    // ... and everyone's; buffer `cur` free
+    if (has_next) mxn = row_max(sn);
+    // V^T transposed reads run 2 MFMAs ahead (2 per MFMA); the row max fills the gaps
+    __builtin_amdgcn_sched_group_barrier(SG_DSR, 4, 1);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 1);
+      if (k < 14) __builtin_amdgcn_sched_group_barrier(SG_DSR, 2, 1);
+      __builtin_amdgcn_sched_group_barrier(SG_VALU, 2, 1);
+    }
+    // K(t+2) and V(t+1) landed (this wave's share; this iteration's DMA may stay in flight)
+    // ... and everyone's; the slots of K(t+1) and V(t) are free after the barrier
+    if (nk && nv && !(ABL & 1)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPT) : "memory");
+    else if ((nk || nv) && !(ABL & 1)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+
+  f32x16 sa[2], sb[2];
+  float mxa = -INFINITY, mxb = -INFINITY;
+  // prologue: K0 V0 K1 needed before iteration 0; V1 K2 stay in flight
+  if (ntiles > 0) { dma_part(0, 0); dma_part(0, 1); }
+  if (ntiles > 1) { dma_part(1, 0); dma_part(1, 1); }
+  if (ntiles > 2) dma_part(2, 0);
+  if (ntiles > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPT) : "memory");
+  else if (ntiles > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPT) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (ntiles > 0) {
+    qk_tile(lds, sa);
+    mask_tile(0, sa);
+    mxa = row_max(sa);
+  }
+  __syncthreads();  // K slot 0 is refilled (tile 3) at the top of iteration 0
+  for (int t = 0; t < ntiles; t += 2) {
+    iter(t, sa, mxa, sb, mxb);
+    if (t + 1 >= ntiles) break;
+    iter(t + 1, sb, mxb, sa, mxa);
   }
 
   // ---- epilogue: normalise, round, gate, store (4 consecutive d per register group)
-  const float lt = l_run + __shfl_xor(l_run, 32, 64);
+  const auto lsw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
+  const float lt = __uint_as_float(lsw[0]) + __uint_as_float(lsw[1]);
   const float inv = 1.0f / lt;
   if (qi >= a.n_q) return;
   bf16_t* op = (bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qi * a.o_ld_tok + head * 128;
@@ -336,8 +721,42 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (a->dtype == ECHO_BF16) {
     if (a->q_ld_tok % 8 || a->o_ld_tok % 4) return ECHO_EALIGN;
-    const int nqb = (a->n_q + QB - 1) / QB;
-    hipLaunchKernelGGL(attn_bf16_kernel, dim3(nqb * a->heads * a->rows), dim3(256), 0, s, *a);
+    static const int abl = [] { const char* e = getenv("ECHO_ATTN_ABL"); return e ? atoi(e) : 0; }();
+    static const int cfg = [] { const char* e = getenv("ECHO_ATTN_CFG"); return e ? atoi(e) : 0; }();
+    const int qb = (cfg == 0 || cfg == 3 || cfg == 5 || cfg == 6) ? 128 : 256;
+    const int nq = (a->n_q + qb - 1) / qb;
+    const dim3 grid(nq * a->heads * a->rows);
+#define ECHO_ATTN_LAUNCH(A, NW, ST, ...) hipLaunchKernelGGL((attn_bf16_kernel<A, NW, ST, ##__VA_ARGS__>), grid, dim3(64 * NW), 0, s, *a)
+#define ECHO_ATTN_ABLS(NW, ST)                        \
+    switch (abl) {                                    \
+      case 1: ECHO_ATTN_LAUNCH(1, NW, ST); break;     \
+      case 2: ECHO_ATTN_LAUNCH(2, NW, ST); break;     \
+      case 3: ECHO_ATTN_LAUNCH(3, NW, ST); break;     \
+      case 4: ECHO_ATTN_LAUNCH(4, NW, ST); break;     \
+      case 6: ECHO_ATTN_LAUNCH(6, NW, ST); break;     \
+      case 7: ECHO_ATTN_LAUNCH(7, NW, ST); break;     \
+      case 8: ECHO_ATTN_LAUNCH(8, NW, ST); break;     \
+      case 13: ECHO_ATTN_LAUNCH(13, NW, ST); break;   \
+      case 19: ECHO_ATTN_LAUNCH(19, NW, ST); break;   \
+      case 35: ECHO_ATTN_LAUNCH(35, NW, ST); break;   \
+      case 51: ECHO_ATTN_LAUNCH(51, NW, ST); break;   \
+      case 64: ECHO_ATTN_LAUNCH(64, NW, ST); break;   \
+      default: ECHO_ATTN_LAUNCH(0, NW, ST); break;    \
+    }
+    if (cfg == 5) {
+      if (abl == 1) hipLaunchKernelGGL(attn_pipe_kernel<1>, grid, dim3(256), 0, s, *a);
+      else hipLaunchKernelGGL(attn_pipe_kernel<0>, grid, dim3(256), 0, s, *a);
+    } else
+    switch (cfg) {
+      case 6: ECHO_ATTN_LAUNCH(0, 4, 2, 32); break;
+      case 3: ECHO_ATTN_ABLS(4, 0); break;
+      case 4: ECHO_ATTN_ABLS(8, 0); break;
+      case 1: ECHO_ATTN_ABLS(8, 2); break;
+      case 2: ECHO_ATTN_ABLS(8, 3); break;
+      default: ECHO_ATTN_ABLS(4, 2); break;
+    }
+#undef ECHO_ATTN_ABLS
+#undef ECHO_ATTN_LAUNCH
   } else if (a->dtype == ECHO_F32) {
     const int nqb = (a->n_q + FQ - 1) / FQ;
     hipLaunchKernelGGL(attn_f32_kernel, dim3(nqb * a->heads * a->rows), dim3(64), 0, s, *a);
