@@ -12,7 +12,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libecho_hip.so")
 
 ECHO_BF16, ECHO_F32 = 0, 1
-EPI_STORE, EPI_SWIGLU, EPI_RESID, EPI_F32OUT = 0, 1, 2, 3
+EPI_STORE, EPI_SWIGLU, EPI_RESID, EPI_F32OUT, EPI_HEADNORM = 0, 1, 2, 3, 4
 ACT_NONE, ACT_SILU = 0, 1
 ERRORS = {-1: "ECHO_EINVAL", -2: "ECHO_EDTYPE", -3: "ECHO_ESHAPE", -4: "ECHO_EALIGN"}
 
@@ -27,7 +27,10 @@ class GemmArgs(C.Structure):
                 ("bias", vp), ("stride_bias", i64),
                 ("aux", vp), ("ld_aux", i64), ("stride_aux", i64),
                 ("gate", vp), ("stride_gate", i64),
-                ("epilogue", i32), ("act", i32), ("out_div", f32), ("tile", i32)]
+                ("epilogue", i32), ("act", i32), ("out_div", f32), ("tile", i32),
+                ("hn_w", vp), ("hn_w_stride", i64), ("hn_rope", vp),
+                ("hn_heads", i32), ("hn_nblk", i32), ("hn_rope_heads", i32), ("hn_seq_len", i32),
+                ("hn_pos0", i32), ("hn_pos_mult", i32), ("hn_eps", f32)]
 
 
 class KVSegment(C.Structure):

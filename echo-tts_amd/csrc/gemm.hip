@@ -29,6 +29,9 @@ struct Epi {
   const void* aux; int64_t ld_aux, stride_aux;
   const void* gate; int64_t stride_gate;
   int epi, act; float out_div;
+  // ECHO_EPI_HEADNORM
+  const void* hn_w; int64_t hn_w_stride; const float* hn_rope;
+  int hn_heads, hn_nblk, hn_rope_heads, hn_seq_len, hn_pos0, hn_pos_mult; float hn_eps;
 };
 
 __device__ __forceinline__ float epi_pointwise(float v, const Epi& ep) {
@@ -41,7 +44,7 @@ __device__ __forceinline__ float epi_pointwise(float v, const Epi& ep) {
 // Epilogue kinds, resolved on the host (ek_of) so the hot GEMMs get straight-line code:
 // EK_GENERIC handles every Epi combination with runtime flags; the specialised kinds cover the
 // decoder's three hot shapes (QKVG store, W13 SwiGLU, Wo/W2 gated residual) without bias/act/div.
-enum { EK_GENERIC = 0, EK_STORE = 1, EK_SWIGLU = 2, EK_RESID = 3 };
+enum { EK_GENERIC = 0, EK_STORE = 1, EK_SWIGLU = 2, EK_RESID = 3, EK_HEADNORM = 4 };
 
 // SiLU for the SwiGLU epilogue: hardware exp2 + reciprocal (≈2 ulp fp32 before the bf16 rounding
 // that follows; the reference's bf16 F.silu rounds the same value, model.py:118-122).
@@ -103,7 +106,55 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
   // ---- epilogue, stage 2: row chunks -> fused row-wise tail -> 16-B stores
   const int Nout = swiglu ? N / 2 : N;
   const int nbase = (swiglu ? n0 / 2 : n0) + wn * TNo;
-  if constexpr (EK != EK_GENERIC) {
+  if constexpr (EK == EK_HEADNORM) {
+    // q/k RMSNorm + RoPE of echo_head_norm_rope fused after the store rounding (256x256 tiles:
+    // a 128-column head spans the staged tiles of waves (wm, 2p) and (wm, 2p+1)). Each wave of
+    // the pair takes 64 of the pair's 128 rows; 16 lanes per row, 8 consecutive columns per lane
+    // and the same xor-butterfly sum as head_norm_rope_kernel, so results are bitwise equal.
+    static_assert(TN == 64 && TM == 128, "HEADNORM epilogue is for the 256x256 kernels");
+    __syncthreads();  // the partner wave's staged tile is complete
+    const int pw = wid & ~1;
+    const int hcol = n0 + (wn & ~1) * TN;  // first column of this pair's head
+    const int hidx = hcol >> 7;
+    const int blk = hidx / ep.hn_heads, h = hidx - blk * ep.hn_heads;
+    const bool norm = blk < ep.hn_nblk;
+    const bool rope = norm && h < ep.hn_rope_heads;
+    const int ch = lane & 15, rq = lane >> 4, c = ch & 7;
+    const bf16_t* src = lds + (pw + (ch >> 3)) * (TM * TN);
+    float wv[8];
+    if (norm) load8((const bf16_t*)ep.hn_w + blk * ep.hn_w_stride + h * 128 + ch * 8, wv);
+    bf16_t* Cp = (bf16_t*)Cv + z * sC + hcol + ch * 8;
+    if (hcol >= N) return;
+    for (int it = 0; it < 16; ++it) {
+      const int row = (wn & 1) * 64 + it * 4 + rq;
+      const int m = m0 + wm * TM + row;
+      float v[8];
+      load8(src + row * TN + ((c ^ (row & 7)) * 8), v);
+      if (norm) {
+        float ss = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ss += v[e] * v[e];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+        const float r = 1.0f / sqrtf(ss / 128.0f + ep.hn_eps);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = rbf((v[e] * r) * wv[e]);
+        if (rope) {
+          const int pos = ep.hn_pos0 + ep.hn_pos_mult * (min(m, M - 1) % ep.hn_seq_len);
+          const float* cs = ep.hn_rope + ((int64_t)pos * 64 + ch * 4) * 2;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float cc = cs[2 * e], sn = cs[2 * e + 1];
+            const float x0 = v[2 * e], x1 = v[2 * e + 1];
+            v[2 * e] = (x0 * cc) - (x1 * sn);
+            v[2 * e + 1] = (x0 * sn) + (x1 * cc);
+          }
+        }
+      }
+      if (m < M) store8(Cp + (int64_t)m * ldc, v);
+    }
+    return;
+  } else if constexpr (EK != EK_GENERIC) {
     // all of this lane's chunks are read (LDS, and the residual rows) before any store, so
     // the long-latency loads overlap; in-place residual (aux == C) is safe because every
     // element is read and written by the same lane.
@@ -708,6 +759,7 @@ int ek_of(const EchoGemmArgs* a) {
     case ECHO_EPI_STORE: return EK_STORE;
     case ECHO_EPI_SWIGLU: return EK_SWIGLU;
     case ECHO_EPI_RESID: return EK_RESID;
+    case ECHO_EPI_HEADNORM: return EK_HEADNORM;
     default: return EK_GENERIC;
   }
 }
@@ -724,6 +776,7 @@ int launch_bf16(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 
 int launch_pp2(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   switch (ek_of(a)) {
+    case EK_HEADNORM: return launch_pp2_ek<EK_HEADNORM>(a, ep, s);
     case EK_STORE: return launch_pp2_ek<EK_STORE>(a, ep, s);
     case EK_SWIGLU: return launch_pp2_ek<EK_SWIGLU>(a, ep, s);
     case EK_RESID: return launch_pp2_ek<EK_RESID>(a, ep, s);
@@ -755,10 +808,29 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   if (a->K % 64 || a->N % 16 || a->lda % 8 || a->ldw % 8 || a->ldc % 8) return ECHO_EALIGN;
   if (a->epilogue == ECHO_EPI_RESID && !a->aux) return ECHO_EINVAL;
   if (a->epilogue == ECHO_EPI_SWIGLU && (a->N % 32 || a->bias)) return ECHO_EINVAL;
-  if (a->epilogue < 0 || a->epilogue > 3) return ECHO_EINVAL;
+  if (a->epilogue < 0 || a->epilogue > 4) return ECHO_EINVAL;
+  const bool headnorm = a->epilogue == ECHO_EPI_HEADNORM;
+  if (headnorm && (a->batch != 1 || !a->hn_w || a->hn_heads <= 0 || a->hn_nblk < 0 || a->hn_seq_len <= 0 ||
+                   (int64_t)a->hn_nblk * a->hn_heads * 128 > a->N || (a->hn_rope_heads > 0 && !a->hn_rope) ||
+                   a->bias || a->act != ECHO_ACT_NONE || a->out_div != 0.0f))
+    return ECHO_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   Epi ep{a->bias, a->stride_bias, a->aux, a->ld_aux, a->stride_aux, a->gate, a->stride_gate,
-         a->epilogue, a->act, a->out_div};
+         a->epilogue, a->act, a->out_div,
+         a->hn_w, a->hn_w_stride, a->hn_rope, a->hn_heads, a->hn_nblk, a->hn_rope_heads, a->hn_seq_len,
+         a->hn_pos0, a->hn_pos_mult, a->hn_eps};
+  int t = a->tile > 0 ? a->tile : pick_tile(a->M, a->N, a->K, a->batch);
+  if (a->tile == 0 && t == 1) t = 13;  // 256x256 tiles run the 2-phase ping-pong (bitwise-identical results)
+  if (headnorm && (a->dtype != ECHO_BF16 || t != 13 || a->N % 128)) {
+    // not fused for this shape / dtype: plain store, then the standalone kernel (same results)
+    EchoGemmArgs b = *a;
+    b.epilogue = ECHO_EPI_STORE;
+    const int rc = echo_gemm(&b, stream);
+    if (rc || a->hn_nblk == 0) return rc;
+    return echo_head_norm_rope(a->dtype, a->C, a->ldc, a->M, a->hn_heads, a->hn_nblk, 0,
+                               (int64_t)a->hn_heads * 128, a->hn_w, a->hn_w_stride, a->hn_rope, a->hn_rope_heads,
+                               a->hn_seq_len, a->hn_pos0, a->hn_pos_mult, a->hn_eps, stream);
+  }
   if (a->dtype == ECHO_F32) {
     dim3 grid((a->N + FT - 1) / FT, (a->M + FT - 1) / FT, a->batch);
     hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, s, (const float*)a->A, a->lda, a->stride_a,
@@ -769,8 +841,6 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   }
   if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
   if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C) & 15) return ECHO_EALIGN;
-  int t = a->tile > 0 ? a->tile : pick_tile(a->M, a->N, a->K, a->batch);
-  if (a->tile == 0 && t == 1) t = 13;  // 256x256 tiles run the 2-phase ping-pong (bitwise-identical results)
   switch (t) {
     case 1: return launch_bf16<256, 256, 2, 4>(a, ep, s);
     case 2: return launch_bf16<256, 128, 4, 2>(a, ep, s);

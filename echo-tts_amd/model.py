@@ -245,9 +245,9 @@ class EchoDiTHip:
         v4 = qkvg.view(B, Lq, 4, h, 128)
         for lay in enc.layers:
             ops.rmsnorm(x, lay.attn_norm, eps, out=xn)
-            ops.gemm(xn, lay.wqkvg, out=qkvg)
-            ops.head_norm_rope(qkvg, h, lay.qk_norm, eps, nblk=2, col0=0, col_stride=Dm, w_stride=h * 128,
-                               rope=self.rope, rope_heads=h, seq_len=Lq)
+            ops.gemm(xn, lay.wqkvg, out=qkvg,
+                     head_norm=ops.HeadNorm(lay.qk_norm, h, 2, eps, w_stride=h * 128, rope=self.rope,
+                                            rope_heads=h, seq_len=Lq))
             ops.attention(v4[:, :, 0], [ops.Segment(v4[:, :, 1], v4[:, :, 2], lens=lens_d, causal=causal)],
                           out=og.view(B, Lq, h, 128), gate=v4[:, :, 3])
             ops.gemm(og, lay.wo, out=x, epilogue=L.EPI_RESID, aux=x)
@@ -404,10 +404,10 @@ class EchoDiTHip:
                 ops.adaln_modulate(ws.h, sh, s1, eps, ws.xn, rows_per_vec=N if per_row_tab else 0,
                                    vec_stride=vstride)
                 if a == 0:
-                    ops.gemm(ws.xn, lay.wqkvg, out=ws.qkvg)
-                    ops.head_norm_rope(ws.qkvg, H, lay.qk_norm, eps, nblk=2, col0=0, col_stride=D,
-                                       w_stride=H * 128, rope=self.rope, rope_heads=H // 2, seq_len=N,
-                                       pos0=start_pos)
+                    # QKVG projection with q/k RMSNorm + half RoPE fused into its epilogue
+                    ops.gemm(ws.xn, lay.wqkvg, out=ws.qkvg,
+                             head_norm=ops.HeadNorm(lay.qk_norm, H, 2, eps, w_stride=H * 128, rope=self.rope,
+                                                    rope_heads=H // 2, seq_len=N, pos0=start_pos))
                     ops.attention(q4[:, :, 0], all_segs, out=og4, gate=q4[:, :, 3])
                     src, w = ws.og, lay.wo
                 else:

@@ -60,11 +60,34 @@ def _mat(t: Tensor, name: str):
     raise ValueError(f"{name}: expected 2-D or 3-D, got {tuple(t.shape)}")
 
 
+@dataclass
+class HeadNorm:
+    """ECHO_EPI_HEADNORM parameters: per-head RMSNorm (+RoPE on heads < rope_heads) of the first
+    nblk column blocks of heads*128 outputs (block b uses w[b*w_stride:]), as in head_norm_rope."""
+    w: Tensor
+    heads: int
+    nblk: int
+    eps: float
+    w_stride: int = 0
+    rope: Optional[Tensor] = None
+    rope_heads: int = 0
+    seq_len: int = 1
+    pos0: int = 0
+    pos_mult: int = 1
+
+
 def gemm(a: Tensor, w: Tensor, out: Optional[Tensor] = None, *, bias: Optional[Tensor] = None,
          epilogue: int = L.EPI_STORE, aux: Optional[Tensor] = None, gate: Optional[Tensor] = None,
-         act: int = L.ACT_NONE, out_div: float = 0.0, tile: int = 0) -> Tensor:
-    """out = epilogue(a @ w^T). a [(B,)M,K], w [(B,)N,K]; see include/echo_hip.h for epilogues."""
-    _check_dev(a, w, out, bias, aux, gate)
+         act: int = L.ACT_NONE, out_div: float = 0.0, tile: int = 0,
+         head_norm: Optional[HeadNorm] = None) -> Tensor:
+    """out = epilogue(a @ w^T). a [(B,)M,K], w [(B,)N,K]; see include/echo_hip.h for epilogues.
+    head_norm selects ECHO_EPI_HEADNORM (fused q/k norm + RoPE after the store rounding)."""
+    _check_dev(a, w, out, bias, aux, gate, None if head_norm is None else head_norm.w,
+               None if head_norm is None else head_norm.rope)
+    if head_norm is not None:
+        if epilogue != L.EPI_STORE:
+            raise ValueError("head_norm replaces the store epilogue")
+        epilogue = L.EPI_HEADNORM
     ba, M, K, lda, sa = _mat(a, "a")
     bw, N, Kw, ldw, sw = _mat(w, "w")
     if Kw != K:
@@ -107,6 +130,13 @@ def gemm(a: Tensor, w: Tensor, out: Optional[Tensor] = None, *, bias: Optional[T
                 raise ValueError("gate must be [(B,)N]")
             args.gate, args.stride_gate = gate.data_ptr(), (gate.stride(0) if gate.dim() == 2 else 0)
     args.epilogue, args.act, args.out_div, args.tile = epilogue, act, out_div, tile
+    if head_norm is not None:
+        hn = head_norm
+        if hn.w.dtype != a.dtype or (hn.rope is not None and hn.rope.dtype != torch.float32):
+            raise TypeError("head_norm weight must be the model dtype, rope table float32")
+        args.hn_w, args.hn_w_stride, args.hn_rope = hn.w.data_ptr(), hn.w_stride, _ptr(hn.rope)
+        args.hn_heads, args.hn_nblk, args.hn_rope_heads = hn.heads, hn.nblk, hn.rope_heads
+        args.hn_seq_len, args.hn_pos0, args.hn_pos_mult, args.hn_eps = hn.seq_len, hn.pos0, hn.pos_mult, hn.eps
     if _DEBUG_SYNC:
         print(f"[echo gemm] M={args.M} N={args.N} K={args.K} batch={args.batch} epi={args.epilogue} "
               f"act={args.act} tile={args.tile} pick={lib().echo_gemm_pick_tile(args.M, args.N, args.K, args.batch)} "

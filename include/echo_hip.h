@@ -39,8 +39,12 @@ enum { ECHO_OK = 0, ECHO_EINVAL = -1, ECHO_EDTYPE = -2, ECHO_ESHAPE = -3, ECHO_E
  *   ECHO_EPI_RESID:  out = round(aux[m][n] + round(gate[n] * v))   gated residual (model.py:385,388)
  *                    (gate NULL: out = round(aux + v); aux may alias out)
  *   ECHO_EPI_F32OUT: out (float32) = v                       out_proj(...).float() (model.py:602-604)
+ *   ECHO_EPI_HEADNORM: out = v, then columns [0, hn_nblk*hn_heads*128) get the per-head
+ *                    RMSNorm (+ RoPE on heads < hn_rope_heads) of echo_head_norm_rope with
+ *                    col0 = 0, col_stride = hn_heads*128 — q_norm/k_norm + RoPE right after
+ *                    the fused QKV(G) projection (model.py:138-142,199-202,221-232); batch == 1
  */
-enum { ECHO_EPI_STORE = 0, ECHO_EPI_SWIGLU = 1, ECHO_EPI_RESID = 2, ECHO_EPI_F32OUT = 3 };
+enum { ECHO_EPI_STORE = 0, ECHO_EPI_SWIGLU = 1, ECHO_EPI_RESID = 2, ECHO_EPI_F32OUT = 3, ECHO_EPI_HEADNORM = 4 };
 enum { ECHO_ACT_NONE = 0, ECHO_ACT_SILU = 1 };
 
 typedef struct {
@@ -56,6 +60,10 @@ typedef struct {
   int32_t epilogue, act;
   float out_div;
   int32_t tile;             /* 0 = auto; else forced config id (tests/tuning) */
+  /* ECHO_EPI_HEADNORM parameters (meaning as in echo_head_norm_rope) */
+  const void* hn_w; int64_t hn_w_stride; const float* hn_rope;
+  int32_t hn_heads, hn_nblk, hn_rope_heads, hn_seq_len, hn_pos0, hn_pos_mult;
+  float hn_eps;
 } EchoGemmArgs;
 
 /* Replaces every nn.Linear of the DiT and its encoders (F.linear, model.py:56-62,

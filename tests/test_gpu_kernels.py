@@ -270,6 +270,36 @@ def test_head_norm_rope(dtype):
     assert torch.equal(x[:, 2 * H * 128:].cpu(), x0[:, 2 * H * 128:])
 
 
+@pytest.mark.parametrize("tile", [0, 13, 2])
+@pytest.mark.parametrize("M,H,pos0", [(333, 4, 5), (1280, 16, 0), (640, 16, 17)])
+def test_gemm_headnorm_fused(tile, M, H, pos0):
+    """ECHO_EPI_HEADNORM == store + echo_head_norm_rope, bitwise (fused in the 2-phase 256x256
+    epilogue for tile 13, composed inside echo_gemm otherwise)."""
+    from echo_tts_amd.model import rope_table_cpu
+    K, N = 256, 4 * H * 128
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    nw = (1 + 0.1 * torch.randn(2, H, 128, device=DEV)).to(BF)
+    rope = rope_table_cpu(128, 4096).to(DEV)
+    seq = 160 if M % 160 == 0 else M
+    ref = ops.gemm(a, w, tile=tile)
+    ops.head_norm_rope(ref, H, nw, 1e-5, nblk=2, col0=0, col_stride=H * 128, w_stride=H * 128, rope=rope,
+                       rope_heads=H // 2, seq_len=seq, pos0=pos0)
+    hn = ops.HeadNorm(nw, H, 2, 1e-5, w_stride=H * 128, rope=rope, rope_heads=H // 2, seq_len=seq, pos0=pos0)
+    got = ops.gemm(a, w, tile=tile, head_norm=hn)
+    assert torch.equal(got, ref)
+
+
+def test_gemm_headnorm_rejects_bad_args():
+    a = torch.randn(64, 64, device=DEV).to(BF)
+    w = torch.randn(512, 64, device=DEV).to(BF)
+    nw = torch.ones(2, 4, 128, device=DEV, dtype=BF)
+    with pytest.raises(RuntimeError):  # 2 blocks x 4 heads x 128 > N
+        ops.gemm(a, w[:512], head_norm=ops.HeadNorm(nw, 4, 2, 1e-5, w_stride=512))
+    with pytest.raises(RuntimeError):  # rope heads without a table
+        ops.gemm(a, w, head_norm=ops.HeadNorm(nw, 2, 2, 1e-5, w_stride=256, rope_heads=1))
+
+
 def test_euler_step_matches_reference_expression():
     from echo_tts_amd import engine as En
     B, N = 2, 50
