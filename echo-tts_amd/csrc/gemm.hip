@@ -107,29 +107,33 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
   const int Nout = swiglu ? N / 2 : N;
   const int nbase = (swiglu ? n0 / 2 : n0) + wn * TNo;
   if constexpr (EK == EK_HEADNORM) {
-    // q/k RMSNorm + RoPE of echo_head_norm_rope fused after the store rounding (256x256 tiles:
-    // a 128-column head spans the staged tiles of waves (wm, 2p) and (wm, 2p+1)). Each wave of
-    // the pair takes 64 of the pair's 128 rows; 16 lanes per row, 8 consecutive columns per lane
-    // and the same xor-butterfly sum as head_norm_rope_kernel, so results are bitwise equal.
-    static_assert(TN == 64 && TM == 128, "HEADNORM epilogue is for the 256x256 kernels");
-    __syncthreads();  // the partner wave's staged tile is complete
-    const int pw = wid & ~1;
-    const int hcol = n0 + (wn & ~1) * TN;  // first column of this pair's head
+    // q/k RMSNorm + RoPE of echo_head_norm_rope fused after the store rounding. A 128-column
+    // head is either one wave's staged tile (TN == 128) or spans the tiles of waves (wm, 2p) and
+    // (wm, 2p+1) (TN == 64; each wave of the pair then takes half of the pair's rows). 16 lanes
+    // per row, 8 consecutive columns per lane and the same xor-butterfly sum as
+    // head_norm_rope_kernel, so results are bitwise equal.
+    static_assert((TN == 64 || TN == 128) && TM == 128, "HEADNORM epilogue is for the 256x256 kernels");
+    constexpr bool PAIR = TN == 64;
+    constexpr int CHS = TN / 8;  // 16-B chunks per staged row
+    if (PAIR) __syncthreads();   // the partner wave's staged tile is complete
+    const int hcol = n0 + (PAIR ? (wn & ~1) : wn) * TN;  // first column of this wave's head
     const int hidx = hcol >> 7;
     const int blk = hidx / ep.hn_heads, h = hidx - blk * ep.hn_heads;
     const bool norm = blk < ep.hn_nblk;
     const bool rope = norm && h < ep.hn_rope_heads;
-    const int ch = lane & 15, rq = lane >> 4, c = ch & 7;
-    const bf16_t* src = lds + (pw + (ch >> 3)) * (TM * TN);
+    const int ch = lane & 15, rq = lane >> 4;
+    const int c = PAIR ? (ch & 7) : ch;
+    const bf16_t* src = lds + (PAIR ? (wid & ~1) + (ch >> 3) : wid) * (TM * TN);
     float wv[8];
     if (norm) load8((const bf16_t*)ep.hn_w + blk * ep.hn_w_stride + h * 128 + ch * 8, wv);
     bf16_t* Cp = (bf16_t*)Cv + z * sC + hcol + ch * 8;
     if (hcol >= N) return;
-    for (int it = 0; it < 16; ++it) {
-      const int row = (wn & 1) * 64 + it * 4 + rq;
+    constexpr int NR = PAIR ? 16 : 32;  // 4-row iterations per wave
+    for (int it = 0; it < NR; ++it) {
+      const int row = (PAIR ? (wn & 1) * 64 : 0) + it * 4 + rq;
       const int m = m0 + wm * TM + row;
       float v[8];
-      load8(src + row * TN + ((c ^ (row & 7)) * 8), v);
+      load8(src + row * TN + ((c ^ (row & (CHS - 1))) * 8), v);
       if (norm) {
         float ss = 0.f;
 #pragma unroll
@@ -159,45 +163,51 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
     // the long-latency loads overlap; in-place residual (aux == C) is safe because every
     // element is read and written by the same lane.
     constexpr int CHc = (EK == EK_SWIGLU ? TN / 2 : TN) / 8, RPIc = 64 / CHc, NIT = TM / RPIc;
+    constexpr int NB = NIT <= 16 ? NIT : 8;  // row chunks in flight per batch (register budget)
     const int c = lane % CHc;
     const int n = nbase + c * 8;
-    u32x4 d[NIT];
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int row = it * RPIc + lane / CHc;
-      d[it] = *(const u32x4*)(stg + row * CHc * 8 + ((c ^ (row & (CHc - 1))) * 8));
-    }
     if (n >= Nout) return;
-    if constexpr (EK == EK_RESID) {
-      float g[8];
-      if (ep.gate) load8((const bf16_t*)ep.gate + z * ep.stride_gate + n, g);
-      const bf16_t* auxp = (const bf16_t*)ep.aux + z * ep.stride_aux + n;
-      u32x4 x[NIT];
-#pragma unroll
-      for (int it = 0; it < NIT; ++it) {
-        const int m = min(m0 + wm * TM + it * RPIc + lane / CHc, M - 1);
-        x[it] = *(const u32x4*)(auxp + (int64_t)m * ep.ld_aux);
-      }
-#pragma unroll
-      for (int it = 0; it < NIT; ++it) {
-        float v[8], xf[8];
-        const bf16_t* dv = (const bf16_t*)&d[it];
-        const bf16_t* xv = (const bf16_t*)&x[it];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          v[e] = bf2f(dv[e]);
-          xf[e] = bf2f(xv[e]);
-          if (ep.gate) v[e] = rbf(g[e] * v[e]);
-          v[e] = xf[e] + v[e];
-        }
-        d[it] = u32x4{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
-      }
-    }
     bf16_t* Cp = (bf16_t*)Cv + z * sC + n;
+    float g[8];
+    if constexpr (EK == EK_RESID) {
+      if (ep.gate) load8((const bf16_t*)ep.gate + z * ep.stride_gate + n, g);
+    }
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int m = m0 + wm * TM + it * RPIc + lane / CHc;
-      if (m < M) *(u32x4*)(Cp + (int64_t)m * ldc) = d[it];
+    for (int i0 = 0; i0 < NIT; i0 += NB) {
+      u32x4 d[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int row = (i0 + b) * RPIc + lane / CHc;
+        d[b] = *(const u32x4*)(stg + row * CHc * 8 + ((c ^ (row & (CHc - 1))) * 8));
+      }
+      if constexpr (EK == EK_RESID) {
+        const bf16_t* auxp = (const bf16_t*)ep.aux + z * ep.stride_aux + n;
+        u32x4 x[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const int m = min(m0 + wm * TM + (i0 + b) * RPIc + lane / CHc, M - 1);
+          x[b] = *(const u32x4*)(auxp + (int64_t)m * ep.ld_aux);
+        }
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          float v[8], xf[8];
+          const bf16_t* dv = (const bf16_t*)&d[b];
+          const bf16_t* xv = (const bf16_t*)&x[b];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            v[e] = bf2f(dv[e]);
+            xf[e] = bf2f(xv[e]);
+            if (ep.gate) v[e] = rbf(g[e] * v[e]);
+            v[e] = xf[e] + v[e];
+          }
+          d[b] = u32x4{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int m = m0 + wm * TM + (i0 + b) * RPIc + lane / CHc;
+        if (m < M) *(u32x4*)(Cp + (int64_t)m * ldc) = d[b];
+      }
     }
     return;
   }

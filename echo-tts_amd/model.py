@@ -479,12 +479,18 @@ def _pair(k: Tensor, v: Tensor) -> Tuple[Tensor, Tensor]:
 
 
 def load_model(path: str, device: str = "cuda", dtype: Optional[torch.dtype] = torch.bfloat16,
-               delete_blockwise_modules: bool = False, cfg: Optional[EchoConfig] = None) -> EchoDiTHip:
-    """`load_model_from_hf` (inference.py:14-69) for a LOCAL safetensors file (no download)."""
+               delete_blockwise_modules: bool = False, cfg: Optional[EchoConfig] = None,
+               lora_path: Optional[str] = None, lora_strength: float = 1.0) -> EchoDiTHip:
+    """`load_model_from_hf` (inference.py:14-69) for a LOCAL safetensors file (no download).
+    lora_path: a reference LoRA checkpoint merged into the weights before they are repacked
+    (gradio_app.py:169-219 + lora.merge_lora_weights; see echo_tts_amd/lora.py)."""
     from .config import FULL
     from .weights import load_state_dict
 
     cfg = cfg or FULL
     dt = dtype or torch.bfloat16
     state = load_state_dict(path, cfg, dt, delete_blockwise_modules)
+    if lora_path is not None:
+        from .lora import apply_lora_checkpoint
+        apply_lora_checkpoint(state, lora_path, lora_strength)
     return EchoDiTHip(cfg, state, device=device, dtype=dt)

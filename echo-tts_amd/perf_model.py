@@ -43,6 +43,38 @@ def sampler_flops(cfg: EchoConfig, N: int, steps_cfg: int, steps_plain: int, tex
     return out
 
 
+def blockwise_flops(cfg: EchoConfig, block_sizes: Sequence[int], steps_cfg: int, steps_plain: int,
+                    text_valid: Sequence[int], spk_valid: Sequence[int]) -> Dict[str, float]:
+    """Algorithmic FLOPs of one blockwise sampler call (inference_blockwise.py:14-123): per block
+    of Nb latents after `start` generated ones, every row-forward also attends to ceil(start/4)
+    latent-prefix patches, and the latent encoder + its K/V projection run once per prompt over
+    that prefix; text/speaker setup once per call."""
+    D, L = cfg.model_size, cfg.num_layers
+    g_tok = gemm_flops_per_token(cfg)
+    a_key = 4 * D * L
+    De, Fe, Le = cfg.text_model_size, cfg.text_intermediate_size, cfg.text_num_layers
+    enc_tok = 2 * Le * (5 * De * De + 3 * De * Fe)
+    out = {"gemm": 0.0, "attention": 0.0, "setup": 0.0, "cond": 0.0}
+    for tv, sv in zip(text_valid, spk_valid):
+        out["setup"] += enc_tok * (tv + sv) + 2 * 2 * De * D * L * (tv + sv)
+        out["setup"] += 4 * De * Le * (tv * tv + sv * (sv + 1) / 2)
+        start = 0
+        for nb in block_sizes:
+            p = -(-start // 4)
+            rows = 3 * steps_cfg + steps_plain
+            keys = (steps_cfg * ((nb + p + tv + sv) + (nb + p + sv) + (nb + p + tv))
+                    + steps_plain * (nb + p + tv + sv))
+            out["gemm"] += rows * nb * g_tok
+            out["attention"] += nb * a_key * keys
+            out["setup"] += enc_tok * p + 2 * 2 * De * D * L * p + 4 * De * Le * p * (p + 1) / 2
+            start += nb
+    S = (steps_cfg + steps_plain) * len(block_sizes)
+    r = cfg.adaln_rank
+    out["cond"] = S * 2 * (cfg.timestep_embed_size * D + D * D + 3 * D * D + 2 * L * 3 * 2 * D * r)
+    out["total"] = sum(out.values())
+    return out
+
+
 class GemmTimer:
     """Wraps ops.gemm: HIP events around every launch of one tile config on the launch
     stream, plus its algorithmic FLOPs (2·M·N·K·batch) — for roofline.achieved."""

@@ -294,18 +294,60 @@ def gen_full(ref_model, ref_inf):
     print("C2-nfe done", time.time() - t0)
 
 
+def gen_lora(ref_model, ref_inf):
+    """LoRA merge pinned to the reference: apply_lora_to_model + seeded adapters +
+    merge_lora_weights (lora.py:99-172,254-272) on the tiny fp32 model, then one CFG forward."""
+    import zlib
+    sys.path.insert(0, REF)
+    import lora as ref_lora  # noqa: E402
+    cfg = C.tiny()
+    m, state = build_ref(ref_model, cfg, torch.float32)
+    rank, alpha = 4, 8.0
+    m, mods = ref_lora.apply_lora_to_model(m, rank=rank, alpha=alpha)
+    out = {}
+    for name, mod in sorted(mods.items()):
+        g = torch.Generator().manual_seed(zlib.crc32(name.encode()))
+        mod.lora_A.data = torch.randn(mod.lora_A.shape, generator=g) * 0.1
+        mod.lora_B.data = torch.randn(mod.lora_B.shape, generator=g) * 0.1
+        out[f"lora.{name}.lora_A"] = mod.lora_A.data.clone()
+        out[f"lora.{name}.lora_B"] = mod.lora_B.data.clone()
+    ref_lora.merge_lora_weights(m)
+    merged = dict(m.state_dict())
+    for k in ("blocks.0.attention.wq.weight", "blocks.1.mlp.w2.weight", "blocks.0.attention.wk_text.weight"):
+        out[f"merged.{k}"] = merged[k].detach().clone()
+    ids, tmask, spk, smask = tiny_inputs(cfg)
+    with torch.inference_mode():
+        kvt = m.get_kv_cache_text(ids, tmask)
+        kvs = m.get_kv_cache_speaker(spk)
+        x = torch.randn((2, 48, 80), generator=torch.Generator().manual_seed(11))
+        t3 = torch.ones(6) * 0.7
+        out["fwd.cfg.v"] = m(x=torch.cat([x, x, x]), t=t3, text_mask=torch.cat([tmask, torch.zeros_like(tmask), tmask]),
+                             speaker_mask=torch.cat([smask, smask, torch.zeros_like(smask)]),
+                             kv_cache_text=ref_inf._concat_kv_caches(kvt, kvt, kvt),
+                             kv_cache_speaker=ref_inf._concat_kv_caches(kvs, kvs, kvs))
+    save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(HERE, "tiny_lora_fp32.safetensors"))
+    with open(os.path.join(HERE, "tiny_lora_fp32.json"), "w") as f:
+        json.dump({"rank": rank, "alpha": alpha, "modules": sorted(mods)}, f, indent=1)
+    print("lora done", len(mods), "modules")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
+    ap.add_argument("--only-lora", action="store_true", help="regenerate only the LoRA fixture")
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count() or 8)
     ref_model, ref_inf, ref_blk = _import_reference()
+    if args.only_lora:
+        gen_lora(ref_model, ref_inf)
+        return
     keys = {"full": ref_key_shapes(ref_model, C.FULL), "tiny": ref_key_shapes(ref_model, C.tiny())}
     with open(os.path.join(HERE, "state_dict_keys.json"), "w") as f:
         json.dump(keys, f)
     gen_host(ref_inf)
     gen_tiny(ref_model, ref_inf, ref_blk, torch.float32, "fp32")
     gen_tiny(ref_model, ref_inf, ref_blk, torch.bfloat16, "bf16")
+    gen_lora(ref_model, ref_inf)
     if not args.skip_full:
         gen_full(ref_model, ref_inf)
 

@@ -59,11 +59,11 @@ __global__ void __launch_bounds__(256) k16(float* out, int iters) {
 }
 
 template <typename K>
-void run(const char* name, K kern, int wgs_per_cu, int flop_per_mfma, int acc) {
+void run(const char* name, K kern, int wgs_per_cu, int flop_per_mfma, int acc, int iters = 4000, int nwg = 0) {
   float* out;
   hipMalloc(&out, 1024 * sizeof(float));
-  const int iters = 4000, cus = 256;
-  dim3 grid(cus * wgs_per_cu), block(256);
+  const int cus = 256;
+  dim3 grid(nwg ? nwg : cus * wgs_per_cu), block(256);
   hipLaunchKernelGGL(kern, grid, block, 0, 0, out, 100);
   hipDeviceSynchronize();
   hipEvent_t e0, e1;
@@ -87,5 +87,8 @@ int main() {
   run("bar/16mfma", k32bar<4>, 2, 32 * 32 * 16 * 2, 4);
   run("bar/64mfma", k32bar<16>, 2, 32 * 32 * 16 * 2, 4);
   run("bar/16mfma", k32bar<4>, 1, 32 * 32 * 16 * 2, 4);
+  // attention-like: 3840 short workgroups of 4 waves, 67 x 4 MFMAs each, barrier every 16
+  run("short-wg", k32bar<4>, 2, 32 * 32 * 16 * 2, 4, 67, 3840);
+  run("long-wg", k32bar<4>, 2, 32 * 32 * 16 * 2, 4, 67 * 15, 256 * 2);
   return 0;
 }
