@@ -717,18 +717,40 @@ constexpr TileCfg kTiles[] = {  // eff: per-tile throughput relative to the 2-ph
     {64, 64, 4, 0.32f},    // 5: 4 waves, 32x32 per wave
 };
 
+// estimated cost of config c (0-based) for an MxN GEMM: rounds x per-CU work / efficiency
+double tile_cost(int c, int M, int N, int batch) {
+  const TileCfg& t = kTiles[c];
+  const double tiles = (double)((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn) * batch;
+  const double rounds = ceil(tiles / (256.0 * t.occ));
+  return rounds * t.occ * (double)t.bm * t.bn / t.eff;
+}
+
 int pick_tile(int M, int N, int K, int batch) {
   (void)K;
   int best = 1;
   double best_t = 1e300;
   for (int c = 0; c < 5; ++c) {
-    const TileCfg& t = kTiles[c];
-    const double tiles = (double)((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn) * batch;
-    const double rounds = ceil(tiles / (256.0 * t.occ));
-    const double est = rounds * t.occ * (double)t.bm * t.bn / t.eff;
+    const double est = tile_cost(c, M, N, batch);
     if (est < best_t * 0.999) { best_t = est; best = c + 1; }
   }
   return best;
+}
+
+// Wave-quantisation split of a 256x256 launch: rows [0, M1) as whole rounds of 256x256 tiles,
+// rows [M1, M) with the cheapest smaller config. Returns M1 (0 = no split) and the tail config.
+int split_rows(int M, int N, int* tail_cfg) {
+  const int tn = (N + 255) / 256;
+  int per = 256;  // rows of 256-row tiles per full round: multiple of 256 / gcd(256, tn)
+  for (int g = tn; g % 2 == 0 && per > 1; g /= 2) per /= 2;
+  const int M1 = (M / (256 * per)) * (256 * per);
+  if (M1 == 0 || M1 >= M) return 0;
+  const double full = tile_cost(0, M, N, 1);
+  double best = 1e300;
+  for (int c = 1; c < 5; ++c) {
+    const double e = tile_cost(c, M - M1, N, 1);
+    if (e < best) { best = e; *tail_cfg = c + 1; }
+  }
+  return tile_cost(0, M1, N, 1) + best < 0.9 * full ? M1 : 0;
 }
 
 template <int BM, int BN, int WM, int WN, int EK>
@@ -851,6 +873,22 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   }
   if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
   if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C) & 15) return ECHO_EALIGN;
+  int tail_cfg = 0;
+  const int M1 = (a->tile == 0 && t == 13 && a->batch == 1 && !headnorm) ? split_rows(a->M, a->N, &tail_cfg) : 0;
+  if (M1 > 0) {
+    // two launches on the same stream: full rounds of the 256x256 kernel, then the row tail
+    EchoGemmArgs h = *a, r = *a;
+    h.M = M1;
+    h.tile = 13;
+    r.M = a->M - M1;
+    r.tile = tail_cfg;
+    r.A = (const bf16_t*)a->A + (int64_t)M1 * a->lda;
+    r.C = (a->epilogue == ECHO_EPI_F32OUT ? (void*)((float*)a->C + (int64_t)M1 * a->ldc)
+                                           : (void*)((bf16_t*)a->C + (int64_t)M1 * a->ldc));
+    if (a->aux) r.aux = (const bf16_t*)a->aux + (int64_t)M1 * a->ld_aux;
+    const int rc = echo_gemm(&h, stream);
+    return rc ? rc : echo_gemm(&r, stream);
+  }
   switch (t) {
     case 1: return launch_bf16<256, 256, 2, 4>(a, ep, s);
     case 2: return launch_bf16<256, 128, 4, 2>(a, ep, s);

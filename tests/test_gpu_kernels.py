@@ -126,6 +126,26 @@ def test_gemm_pingpong_bitwise(M, N, K):
     assert torch.equal(ref, ops.gemm(a, w, tile=13))
 
 
+@pytest.mark.parametrize("epi", [L.EPI_STORE, L.EPI_RESID, L.EPI_F32OUT])
+def test_gemm_row_split_bitwise(epi):
+    """Auto-tiled 10240x2048 launches split rows into whole 256x256 rounds + a smaller-tile tail;
+    the result (including the in-place residual's row offsets) is bitwise the unsplit launch."""
+    M, N, K = 10240, 2048, 128
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    g = torch.tanh(torch.randn(N, device=DEV)).to(BF)
+    h = torch.randn(M, N, device=DEV).to(BF)
+    outs = []
+    for tile in (0, 13):
+        if epi == L.EPI_RESID:
+            o = h.clone()
+            ops.gemm(a, w, out=o, epilogue=epi, aux=o, gate=g, tile=tile)
+        else:
+            o = ops.gemm(a, w, epilogue=epi, tile=tile)
+        outs.append(o)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_gemm_f32():
     M, N, K = 130, 96, 192
     a = torch.randn(M, K, device=DEV)
