@@ -19,6 +19,10 @@
 // conflict-free for both the K row reads and the V transposed reads.
 #include "common.h"
 
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
 namespace {
 
 __device__ __forceinline__ int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
@@ -44,6 +48,11 @@ __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
 
 constexpr int KT = 64;   // keys per tile
 
+// Diagnostics only (ECHO_ATTN_ABL bit 128, tools/attn_timeline.py): per-workgroup s_memrealtime
+// stamps [entry, prologue landed, tile loop done, exit, ntiles, XCD] written by wave 0, lane 0.
+__device__ uint64_t* g_attn_stamps;
+__device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+
 // value select (a ?: between two named variables is an lvalue: clang selects their ADDRESSES,
 // which keeps SROA from promoting them and sends them to scratch)
 template <class T>
@@ -68,6 +77,7 @@ template <int ABL, int NW, int ST, int KTT = 64>
 __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) attn_bf16_kernel(EchoAttnArgs a) {
   constexpr int QB = 32 * NW;
   constexpr int DPT = KTT / (4 * NW);  // DMA wave-instructions per wave per K (or V) tile
+  const uint64_t ts0 = (ABL & 128) ? rt_now() : 0;
   constexpr int NKK = KTT / 32;        // 32-key sub-tiles per tile
   // [stage][K | V][64 keys x 128] — one array (keeps hipcc from draining DMA before ds_reads)
   constexpr int NBUF = ST == 0 ? 2 : ST;
@@ -206,6 +216,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
   }
   __syncthreads();
 
+  const uint64_t ts1 = (ABL & 128) ? rt_now() : 0;
   int cur = 0;
   if (ABL & 64) ntiles = 0;
   for (int ti = 0; ti < ntiles; ++ti) {
@@ -328,6 +339,11 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
     }
   }
 
+  const uint64_t ts2 = (ABL & 128) ? rt_now() : 0;
+  if ((ABL & 128) && threadIdx.x == 0) {
+    uint64_t* st = g_attn_stamps + (int64_t)blockIdx.x * 6;
+    st[0] = ts0; st[1] = ts1; st[2] = ts2; st[4] = ntiles; st[5] = blockIdx.x & 7;
+  }
   // ---- epilogue: normalise, round, gate, store (4 consecutive d per register group)
   const float lt = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = 1.0f / lt;
@@ -335,6 +351,13 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
   bf16_t* op = (bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qi * a.o_ld_tok + head * 128;
   const bf16_t* gp = a.gate ? (const bf16_t*)a.gate + row * a.g_ld_batch + (int64_t)qi * a.g_ld_tok + head * 128
                             : nullptr;
+  // all 16 gate loads first: gate and out may alias as far as the compiler knows, so loads
+  // interleaved with the stores would serialise 16 memory latencies (≈10 us per workgroup)
+  uint2 gg[16];
+  if (gp) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) gg[k] = *(const uint2*)(gp + (k >> 2) * 32 + 8 * (k & 3) + 4 * h2);
+  }
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -344,13 +367,17 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = rbf(o[dt][4 * rg + e] * inv);
       if (gp) {
-        const uint2 gg = *(const uint2*)(gp + d);
-        const float gv[4] = {bf2f(gg.x & 0xffffu), bf2f(gg.x >> 16), bf2f(gg.y & 0xffffu), bf2f(gg.y >> 16)};
+        const uint2 g2 = gg[dt * 4 + rg];
+        const float gv[4] = {bf2f(g2.x & 0xffffu), bf2f(g2.x >> 16), bf2f(g2.y & 0xffffu), bf2f(g2.y >> 16)};
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = rbf(v[e] * rbf(sigmoid_f(gv[e])));
       }
       *(uint2*)(op + d) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
     }
+  if ((ABL & 128) && threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    g_attn_stamps[(int64_t)blockIdx.x * 6 + 3] = rt_now();
+  }
 }
 
 // ----------------------------------------------------------------------------- software-pipelined
@@ -622,6 +649,13 @@ __global__ void __launch_bounds__(256, 1) attn_pipe_kernel(EchoAttnArgs a) {
   bf16_t* op = (bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qi * a.o_ld_tok + head * 128;
   const bf16_t* gp = a.gate ? (const bf16_t*)a.gate + row * a.g_ld_batch + (int64_t)qi * a.g_ld_tok + head * 128
                             : nullptr;
+  // all 16 gate loads first: gate and out may alias as far as the compiler knows, so loads
+  // interleaved with the stores would serialise 16 memory latencies (≈10 us per workgroup)
+  uint2 gg[16];
+  if (gp) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) gg[k] = *(const uint2*)(gp + (k >> 2) * 32 + 8 * (k & 3) + 4 * h2);
+  }
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -631,8 +665,8 @@ __global__ void __launch_bounds__(256, 1) attn_pipe_kernel(EchoAttnArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = rbf(o[dt][4 * rg + e] * inv);
       if (gp) {
-        const uint2 gg = *(const uint2*)(gp + d);
-        const float gv[4] = {bf2f(gg.x & 0xffffu), bf2f(gg.x >> 16), bf2f(gg.y & 0xffffu), bf2f(gg.y >> 16)};
+        const uint2 g2 = gg[dt * 4 + rg];
+        const float gv[4] = {bf2f(g2.x & 0xffffu), bf2f(g2.x >> 16), bf2f(g2.y & 0xffffu), bf2f(g2.y >> 16)};
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = rbf(v[e] * rbf(sigmoid_f(gv[e])));
       }
@@ -723,9 +757,19 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
     if (a->q_ld_tok % 8 || a->o_ld_tok % 4) return ECHO_EALIGN;
     static const int abl = [] { const char* e = getenv("ECHO_ATTN_ABL"); return e ? atoi(e) : 0; }();
     static const int cfg = [] { const char* e = getenv("ECHO_ATTN_CFG"); return e ? atoi(e) : 0; }();
-    const int qb = (cfg == 0 || cfg == 3 || cfg == 5 || cfg == 6) ? 128 : 256;
+    const int qb = (cfg == 0 || cfg == 3 || cfg == 5 || cfg == 6 || cfg == 7) ? 128 : 256;
     const int nq = (a->n_q + qb - 1) / qb;
     const dim3 grid(nq * a->heads * a->rows);
+    static uint64_t* stamps = nullptr;
+    static size_t stamps_n = 0;
+    if (abl & 128) {  // diagnostics: per-workgroup timeline (see g_attn_stamps)
+      if (stamps_n < (size_t)grid.x * 6) {
+        if (stamps) (void)hipFree(stamps);
+        stamps_n = (size_t)grid.x * 6;
+        if (hipMalloc(&stamps, stamps_n * 8) != hipSuccess) return ECHO_EINVAL;
+      }
+      if (hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), &stamps, sizeof(stamps)) != hipSuccess) return ECHO_EINVAL;
+    }
 #define ECHO_ATTN_LAUNCH(A, NW, ST, ...) hipLaunchKernelGGL((attn_bf16_kernel<A, NW, ST, ##__VA_ARGS__>), grid, dim3(64 * NW), 0, s, *a)
 #define ECHO_ATTN_ABLS(NW, ST)                        \
     switch (abl) {                                    \
@@ -741,6 +785,7 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
       case 35: ECHO_ATTN_LAUNCH(35, NW, ST); break;   \
       case 51: ECHO_ATTN_LAUNCH(51, NW, ST); break;   \
       case 64: ECHO_ATTN_LAUNCH(64, NW, ST); break;   \
+      case 128: ECHO_ATTN_LAUNCH(128, NW, ST); break; \
       default: ECHO_ATTN_LAUNCH(0, NW, ST); break;    \
     }
     if (cfg == 5) {
@@ -749,6 +794,7 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
     } else
     switch (cfg) {
       case 6: ECHO_ATTN_LAUNCH(0, 4, 2, 32); break;
+      case 7: ECHO_ATTN_LAUNCH(0, 4, 3, 32); break;
       case 3: ECHO_ATTN_ABLS(4, 0); break;
       case 4: ECHO_ATTN_ABLS(8, 0); break;
       case 1: ECHO_ATTN_ABLS(8, 2); break;
@@ -757,6 +803,18 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
     }
 #undef ECHO_ATTN_ABLS
 #undef ECHO_ATTN_LAUNCH
+    if (abl & 128) {  // dump this call's timeline (overwrites: the last call wins)
+      const char* path = getenv("ECHO_ATTN_STAMPS");
+      if (path && hipStreamSynchronize(s) == hipSuccess) {
+        std::vector<uint64_t> h((size_t)grid.x * 6);
+        if (hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+          if (FILE* f = fopen(path, "wb")) {
+            fwrite(h.data(), 8, h.size(), f);
+            fclose(f);
+          }
+        }
+      }
+    }
   } else if (a->dtype == ECHO_F32) {
     const int nqb = (a->n_q + FQ - 1) / FQ;
     hipLaunchKernelGGL(attn_f32_kernel, dim3(nqb * a->heads * a->rows), dim3(64), 0, s, *a);

@@ -25,10 +25,17 @@ def timeit(fn, iters=10, rounds=5):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=0, help="only this row count (48 = CFG, 16 = plain)")
+    ap.add_argument("--real-only", action="store_true")
+    args = ap.parse_args()
     dev = "cuda"
     B, N, H, T, P = 16, 640, 16, 448, 160
     for R, tl_c, sl_c in ((3 * B, [388] * B + [0] * B + [388] * B, [160] * 2 * B + [0] * B),
                           (B, [388] * B, [160] * B)):
+        if args.rows and R != args.rows:
+            continue
         qkvg = (torch.randn(R, N, 4, H, 128, device=dev)).to(torch.bfloat16)
         kt = torch.randn(B, T, 24, 2, H, 128, device=dev).to(torch.bfloat16)[:, :, 3]
         ks = torch.randn(B, P, 24, 2, H, 128, device=dev).to(torch.bfloat16)[:, :, 3]
@@ -37,7 +44,7 @@ def main():
         out = torch.empty(R, N, H, 128, device=dev, dtype=torch.bfloat16)
         keys = sum(N + t + s for t, s in zip(tl_c, sl_c))
         fl = 4.0 * N * keys * 128 * H
-        for name, bm_self, bm_c in (("real", None, B), ("shared-kv", 1, 1)):
+        for name, bm_self, bm_c in (("real", None, B), ("shared-kv", 1, 1))[: 1 if args.real_only else 2]:
             segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2], batch_mod=bm_self),
                     ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=bm_c),
                     ops.Segment(ks[:, :, 0], ks[:, :, 1], lens=sl, batch_mod=bm_c)]
