@@ -19,10 +19,6 @@
 // conflict-free for both the K row reads and the V transposed reads.
 #include "common.h"
 
-#include <cstdio>
-#include <cstdlib>
-#include <vector>
-
 namespace {
 
 __device__ __forceinline__ int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
@@ -48,7 +44,7 @@ __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
 
 constexpr int KT = 64;   // keys per tile
 
-// Diagnostics only (ECHO_ATTN_ABL bit 128, tools/attn_timeline.py): per-workgroup s_memrealtime
+// Diagnostics only (echo_attention_variant ablation bit 128, tools/attn_timeline.py): s_memrealtime
 // stamps [entry, prologue landed, tile loop done, exit, ntiles, XCD] written by wave 0, lane 0.
 __device__ uint64_t* g_attn_stamps;
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
@@ -67,7 +63,7 @@ struct SegInfo {
   int kend, causal, first;  // first = index of the segment's first tile in the flat tile list
 };
 
-// ABL: timing ablations only (tools/bench_attn.py via ECHO_ATTN_ABL; results are wrong):
+// ABL: timing ablations only (echo_attention_variant, tools/bench_attn.py; results are wrong):
 // 1 = no in-loop DMA, 2 = no softmax VALU, 4 = no PV (MFMA + V reads), 8 = no QK (MFMA + K reads)
 // NW waves x 32 queries per workgroup (QB = 32 NW). K/V staging: ST = 2 or 3 -> ST-stage LDS ring
 // filled by LDS-DMA (tile t+ST-1 issued at tile t); ST = 0 -> register staging (cdna_hip_programming.md
@@ -237,6 +233,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
 
     // ---- S^T = K . Q^T for two 32-key sub-tiles
     f32x16 st[NKK];
+    if (ABL & 256) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
 #pragma unroll
@@ -253,6 +250,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
         st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], st[kk], 0, 0, 0);
       }
     }
+    if (ABL & 256) __builtin_amdgcn_s_setprio(0);
     // ---- mask (partial tiles only), online softmax (lane = query, registers = keys).
     // The running max is kept on RAW scores (scale > 0 preserves the argmax); one FMA per score
     // forms the exp2 argument s*c - m*c; raw v_exp_f32 (results < 2^-126 flush to 0).
@@ -296,6 +294,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
     m_run = m_new;
     }
 
+    if (ABL & 256) __builtin_amdgcn_s_setprio(1);
     // ---- O^T += V^T . P  (P from the accumulators, V^T by transposed LDS reads)
 #pragma unroll
     for (int kk = 0; kk < ((ABL & 4) ? 0 : NKK); ++kk)
@@ -327,6 +326,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
           o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf, o[dt], 0, 0, 0);
         }
       }
+    if (ABL & 256) __builtin_amdgcn_s_setprio(0);
     if constexpr (ST == 0) {
       __syncthreads();  // tile ti+1 was written at the top of this tile
       cur ^= 1;
@@ -740,7 +740,9 @@ __global__ void __launch_bounds__(64) attn_f32_kernel(EchoAttnArgs a) {
 
 }  // namespace
 
-extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
+namespace {
+
+int check_attn_args(const EchoAttnArgs* a) {
   if (!a || !a->q || !a->out) return ECHO_EINVAL;
   if (a->rows <= 0 || a->n_q <= 0 || a->heads <= 0 || a->nseg < 1 || a->nseg > 4) return ECHO_ESHAPE;
   bool any = false;
@@ -752,75 +754,86 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
     any = true;
   }
   if (!any) return ECHO_EINVAL;
-  hipStream_t s = (hipStream_t)stream;
-  if (a->dtype == ECHO_BF16) {
-    if (a->q_ld_tok % 8 || a->o_ld_tok % 4) return ECHO_EALIGN;
-    static const int abl = [] { const char* e = getenv("ECHO_ATTN_ABL"); return e ? atoi(e) : 0; }();
-    static const int cfg = [] { const char* e = getenv("ECHO_ATTN_CFG"); return e ? atoi(e) : 0; }();
-    const int qb = (cfg == 0 || cfg == 3 || cfg == 5 || cfg == 6 || cfg == 7) ? 128 : 256;
-    const int nq = (a->n_q + qb - 1) / qb;
-    const dim3 grid(nq * a->heads * a->rows);
-    static uint64_t* stamps = nullptr;
-    static size_t stamps_n = 0;
-    if (abl & 128) {  // diagnostics: per-workgroup timeline (see g_attn_stamps)
-      if (stamps_n < (size_t)grid.x * 6) {
-        if (stamps) (void)hipFree(stamps);
-        stamps_n = (size_t)grid.x * 6;
-        if (hipMalloc(&stamps, stamps_n * 8) != hipSuccess) return ECHO_EINVAL;
-      }
-      if (hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), &stamps, sizeof(stamps)) != hipSuccess) return ECHO_EINVAL;
-    }
+  if (a->dtype == ECHO_BF16 && (a->q_ld_tok % 8 || a->o_ld_tok % 4)) return ECHO_EALIGN;
+  if (a->dtype != ECHO_BF16 && a->dtype != ECHO_F32) return ECHO_EDTYPE;
+  return 0;
+}
+
+int attn_grid(const EchoAttnArgs* a, int qb) { return ((a->n_q + qb - 1) / qb) * a->heads * a->rows; }
+
+// Measurement variants of the bf16 kernel (tools/bench_attn.py; DESIGN.md §7 lists what each
+// showed). variant: 0 production (4 waves, 2-slot LDS-DMA ring, 64-key tiles), 1/2 8 waves with
+// a 2/3-slot ring, 3/4 register-staged K/V with 4/8 waves, 5 software-pipelined one-wave-per-SIMD
+// kernel, 6/7 32-key tiles with a 2/3-slot ring. ablation: the ABL bits of attn_bf16_kernel.
+int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) {
+  const int qb = (cfg == 0 || cfg == 3 || cfg == 5 || cfg == 6 || cfg == 7) ? 128 : 256;
+  const dim3 grid(attn_grid(a, qb));
 #define ECHO_ATTN_LAUNCH(A, NW, ST, ...) hipLaunchKernelGGL((attn_bf16_kernel<A, NW, ST, ##__VA_ARGS__>), grid, dim3(64 * NW), 0, s, *a)
 #define ECHO_ATTN_ABLS(NW, ST)                        \
-    switch (abl) {                                    \
-      case 1: ECHO_ATTN_LAUNCH(1, NW, ST); break;     \
-      case 2: ECHO_ATTN_LAUNCH(2, NW, ST); break;     \
-      case 3: ECHO_ATTN_LAUNCH(3, NW, ST); break;     \
-      case 4: ECHO_ATTN_LAUNCH(4, NW, ST); break;     \
-      case 6: ECHO_ATTN_LAUNCH(6, NW, ST); break;     \
-      case 7: ECHO_ATTN_LAUNCH(7, NW, ST); break;     \
-      case 8: ECHO_ATTN_LAUNCH(8, NW, ST); break;     \
-      case 13: ECHO_ATTN_LAUNCH(13, NW, ST); break;   \
-      case 19: ECHO_ATTN_LAUNCH(19, NW, ST); break;   \
-      case 35: ECHO_ATTN_LAUNCH(35, NW, ST); break;   \
-      case 51: ECHO_ATTN_LAUNCH(51, NW, ST); break;   \
-      case 64: ECHO_ATTN_LAUNCH(64, NW, ST); break;   \
-      case 128: ECHO_ATTN_LAUNCH(128, NW, ST); break; \
-      default: ECHO_ATTN_LAUNCH(0, NW, ST); break;    \
-    }
-    if (cfg == 5) {
+  switch (abl) {                                      \
+    case 0: ECHO_ATTN_LAUNCH(0, NW, ST); break;       \
+    case 1: ECHO_ATTN_LAUNCH(1, NW, ST); break;       \
+    case 2: ECHO_ATTN_LAUNCH(2, NW, ST); break;       \
+    case 3: ECHO_ATTN_LAUNCH(3, NW, ST); break;       \
+    case 4: ECHO_ATTN_LAUNCH(4, NW, ST); break;       \
+    case 6: ECHO_ATTN_LAUNCH(6, NW, ST); break;       \
+    case 7: ECHO_ATTN_LAUNCH(7, NW, ST); break;       \
+    case 8: ECHO_ATTN_LAUNCH(8, NW, ST); break;       \
+    case 13: ECHO_ATTN_LAUNCH(13, NW, ST); break;     \
+    case 19: ECHO_ATTN_LAUNCH(19, NW, ST); break;     \
+    case 35: ECHO_ATTN_LAUNCH(35, NW, ST); break;     \
+    case 51: ECHO_ATTN_LAUNCH(51, NW, ST); break;     \
+    case 64: ECHO_ATTN_LAUNCH(64, NW, ST); break;     \
+    case 128: ECHO_ATTN_LAUNCH(128, NW, ST); break;   \
+    case 256: ECHO_ATTN_LAUNCH(256, NW, ST); break;   \
+    default: return ECHO_EINVAL;                      \
+  }
+  switch (cfg) {
+    case 0: ECHO_ATTN_ABLS(4, 2); break;
+    case 1: ECHO_ATTN_ABLS(8, 2); break;
+    case 2: ECHO_ATTN_ABLS(8, 3); break;
+    case 3: ECHO_ATTN_ABLS(4, 0); break;
+    case 4: ECHO_ATTN_ABLS(8, 0); break;
+    case 5:
       if (abl == 1) hipLaunchKernelGGL(attn_pipe_kernel<1>, grid, dim3(256), 0, s, *a);
-      else hipLaunchKernelGGL(attn_pipe_kernel<0>, grid, dim3(256), 0, s, *a);
-    } else
-    switch (cfg) {
-      case 6: ECHO_ATTN_LAUNCH(0, 4, 2, 32); break;
-      case 7: ECHO_ATTN_LAUNCH(0, 4, 3, 32); break;
-      case 3: ECHO_ATTN_ABLS(4, 0); break;
-      case 4: ECHO_ATTN_ABLS(8, 0); break;
-      case 1: ECHO_ATTN_ABLS(8, 2); break;
-      case 2: ECHO_ATTN_ABLS(8, 3); break;
-      default: ECHO_ATTN_ABLS(4, 2); break;
-    }
+      else if (abl == 0) hipLaunchKernelGGL(attn_pipe_kernel<0>, grid, dim3(256), 0, s, *a);
+      else return ECHO_EINVAL;
+      break;
+    case 6: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 2, 32); break;
+    case 7: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 3, 32); break;
+    default: return ECHO_EINVAL;
+  }
 #undef ECHO_ATTN_ABLS
 #undef ECHO_ATTN_LAUNCH
-    if (abl & 128) {  // dump this call's timeline (overwrites: the last call wins)
-      const char* path = getenv("ECHO_ATTN_STAMPS");
-      if (path && hipStreamSynchronize(s) == hipSuccess) {
-        std::vector<uint64_t> h((size_t)grid.x * 6);
-        if (hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-          if (FILE* f = fopen(path, "wb")) {
-            fwrite(h.data(), 8, h.size(), f);
-            fclose(f);
-          }
-        }
-      }
-    }
-  } else if (a->dtype == ECHO_F32) {
-    const int nqb = (a->n_q + FQ - 1) / FQ;
-    hipLaunchKernelGGL(attn_f32_kernel, dim3(nqb * a->heads * a->rows), dim3(64), 0, s, *a);
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
+  const int rc = check_attn_args(a);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if (a->dtype == ECHO_BF16) {
+    hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a);
   } else {
-    return ECHO_EDTYPE;
+    hipLaunchKernelGGL(attn_f32_kernel, dim3(attn_grid(a, FQ)), dim3(64), 0, s, *a);
   }
   ECHO_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int echo_attention_variant(const EchoAttnArgs* a, int32_t variant, int32_t ablation, uint64_t* stamps,
+                                      void* stream) {
+  const int rc = check_attn_args(a);
+  if (rc) return rc;
+  if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
+  if ((ablation & 128) && (!stamps || variant > 4)) return ECHO_EINVAL;  // stamps: attn_bf16_kernel variants
+  if (ablation & 128) {
+    if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_attn_stamps), &stamps, sizeof(stamps), 0, hipMemcpyHostToDevice,
+                               (hipStream_t)stream) != hipSuccess)
+      return ECHO_EINVAL;
+  }
+  return launch_attn_variant(a, variant, ablation, (hipStream_t)stream);
 }

@@ -164,9 +164,8 @@ def _head_view(t: Tensor, name: str):
     return t.stride(1), t.stride(0)
 
 
-def attention(q: Tensor, segments: Sequence[Segment], out: Tensor, gate: Optional[Tensor] = None,
-              scale: float = 128 ** -0.5) -> Tensor:
-    """out = softmax(q.K^T * scale) V over the concatenated segments, * sigmoid(gate)."""
+def _attn_args(q: Tensor, segments: Sequence[Segment], out: Tensor, gate: Optional[Tensor],
+               scale: float) -> "L.AttnArgs":
     _check_dev(q, out, gate)
     if len(segments) > 4 or not segments:
         raise ValueError("1-4 segments")
@@ -206,7 +205,25 @@ def attention(q: Tensor, segments: Sequence[Segment], out: Tensor, gate: Optiona
         seg.causal = int(s.causal)
         if s.k.shape[1] == 0:
             seg.k = None
+    return a
+
+
+def attention(q: Tensor, segments: Sequence[Segment], out: Tensor, gate: Optional[Tensor] = None,
+              scale: float = 128 ** -0.5) -> Tensor:
+    """out = softmax(q.K^T * scale) V over the concatenated segments, * sigmoid(gate)."""
+    a = _attn_args(q, segments, out, gate, scale)
     L.check(lib().echo_attention(C.byref(a), _stream()), "echo_attention")
+    return out
+
+
+def attention_variant(q: Tensor, segments: Sequence[Segment], out: Tensor, gate: Optional[Tensor] = None,
+                      scale: float = 128 ** -0.5, *, variant: int = 0, ablation: int = 0,
+                      stamps: Optional[Tensor] = None) -> Tensor:
+    """Diagnostics only (echo_attention_variant): measurement variants / ablations of the bf16
+    attention kernel; with ablation bit 128, `stamps` (int64 [workgroups, 6]) gets the timeline."""
+    a = _attn_args(q, segments, out, gate, scale)
+    L.check(lib().echo_attention_variant(C.byref(a), variant, ablation, _ptr(stamps), _stream()),
+            "echo_attention_variant")
     return out
 
 

@@ -99,6 +99,14 @@ typedef struct {
  * JointAttention.forward (model.py:237-264) and SelfAttention.forward (model.py:144-157). */
 int echo_attention(const EchoAttnArgs* args, void* stream);
 
+/* Diagnostics only (tools/bench_attn.py, tools/attn_timeline.py; never on the sampling path):
+ * measurement variants of the bf16 attention kernel. variant 0 = the production kernel;
+ * ablation != 0 removes parts of the work (results are then WRONG, timing only); ablation bit 128
+ * records per-workgroup s_memrealtime stamps into `stamps` (device, [workgroups][6] uint64:
+ * entry, prologue landed, tile loop done, exit, tiles, XCD). Variants/bits: csrc/attention.hip. */
+int echo_attention_variant(const EchoAttnArgs* args, int32_t variant, int32_t ablation, uint64_t* stamps,
+                           void* stream);
+
 /* RMSNorm(x)*w in fp32, cast back (model.py:99-104). Row stride in elements. */
 int echo_rmsnorm(int32_t dtype, const void* x, int64_t ldx, const void* w, void* y, int64_t ldy,
                  int32_t rows, int32_t dim, float eps, void* stream);

@@ -199,6 +199,34 @@ def ref_attention(q, segs, gate, scale, dtype):
     return o
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+def test_attention_variants_match_production(variant):
+    """Diagnostic entry point: every measurement variant computes the production result
+    (variant 0 bitwise; the others up to accumulation-order rounding), and the timeline
+    stamps are written."""
+    B, N, H = 2, 200, 4
+    R = 3 * B
+    qkvg = torch.randn(R, N, 4, H, 128, device=DEV).to(BF)
+    kt = torch.randn(B, 96, 2, H, 128, device=DEV).to(BF)
+    tl = torch.tensor([50, 71, 0, 0, 50, 71], dtype=torch.int32, device=DEV)
+    segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2]), ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=B)]
+    ref = torch.empty(R, N, H, 128, device=DEV, dtype=BF)
+    ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
+    got = torch.empty_like(ref)
+    ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=variant)
+    if variant == 0:
+        assert torch.equal(got, ref)
+    else:
+        close_bf16(got, ref.float().cpu())
+    if variant <= 4:
+        st = torch.zeros((2 * R * H * 2, 6), device=DEV, dtype=torch.int64)
+        ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=variant, ablation=128,
+                              stamps=st)
+        torch.cuda.synchronize()
+        n = ((N + 32 * (4 if variant in (0, 3) else 8) - 1) // (32 * (4 if variant in (0, 3) else 8))) * H * R
+        assert (st[:n, 3] >= st[:n, 0]).all() and (st[:n, 0] > 0).all()
+
+
 @pytest.mark.parametrize("dtype", [BF, torch.float32])
 def test_attention_segments(dtype):
     B, N, H = 2, 200, 4

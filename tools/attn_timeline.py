@@ -1,12 +1,13 @@
-"""Per-workgroup attention timeline from ECHO_ATTN_ABL=128 stamps (s_memrealtime, 100 MHz).
-    ECHO_ATTN_ABL=128 ECHO_ATTN_STAMPS=/tmp/st.bin python tools/bench_attn.py; python tools/attn_timeline.py /tmp/st.bin"""
+"""Per-workgroup attention timeline from ablation-128 stamps (s_memrealtime, 100 MHz).
+    python tools/bench_attn.py --rows 48 --real-only --ablation 128 --stamps /tmp/st.npy
+    python tools/attn_timeline.py /tmp/st.npy"""
 import sys
 
 import numpy as np
 
 
 def main():
-    a = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 6).astype(np.int64)
+    a = np.load(sys.argv[1]).reshape(-1, 6).astype(np.int64)
     t0 = a[:, 0].min()
     ent, pro, loop, ext = (a[:, i] - t0 for i in range(4))
     nt = a[:, 4]

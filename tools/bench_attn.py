@@ -29,6 +29,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=0, help="only this row count (48 = CFG, 16 = plain)")
     ap.add_argument("--real-only", action="store_true")
+    ap.add_argument("--variant", type=int, default=None, help="echo_attention_variant variant id (diagnostics)")
+    ap.add_argument("--ablation", type=int, default=0, help="ablation bits (timing only, results wrong)")
+    ap.add_argument("--stamps", default=None, help="ablation 128: write the last call's timeline (.npy)")
     args = ap.parse_args()
     dev = "cuda"
     B, N, H, T, P = 16, 640, 16, 448, 160
@@ -48,7 +51,18 @@ def main():
             segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2], batch_mod=bm_self),
                     ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=bm_c),
                     ops.Segment(ks[:, :, 0], ks[:, :, 1], lens=sl, batch_mod=bm_c)]
-            ms = timeit(lambda: ops.attention(qkvg[:, :, 0], segs, out=out, gate=qkvg[:, :, 3]))
+            if args.variant is None and not args.ablation:
+                fn = lambda: ops.attention(qkvg[:, :, 0], segs, out=out, gate=qkvg[:, :, 3])  # noqa: E731
+            else:
+                nwg = ((N + 127) // 128) * H * R * 2  # upper bound over variants (QB >= 128)
+                st = torch.zeros((nwg, 6), device=dev, dtype=torch.int64) if args.ablation & 128 else None
+                fn = lambda: ops.attention_variant(qkvg[:, :, 0], segs, out=out, gate=qkvg[:, :, 3],  # noqa: E731
+                                                   variant=args.variant or 0, ablation=args.ablation, stamps=st)
+            ms = timeit(fn)
+            if args.stamps and args.ablation & 128:
+                import numpy as np
+                n = ((N + 127) // 128) * H * R
+                np.save(args.stamps, st[:n].cpu().numpy())
             print(f"R={R:3d} {name:10s} {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TFLOP/s", flush=True)
 
 
