@@ -38,6 +38,13 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
                : "=&s"(keep) : "v"(gsrc), "s"(lds_addr) : "memory");
 }
 
+// SADDR form: address = 64-bit scalar base + 32-bit per-lane byte offset (no 64-bit VALU math)
+__device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_addr) : "memory");
+}
+
 __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
@@ -48,6 +55,15 @@ constexpr int KT = 64;   // keys per tile
 // stamps [entry, prologue landed, tile loop done, exit, ntiles, XCD] written by wave 0, lane 0.
 __device__ uint64_t* g_attn_stamps;
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+// bit 512: per-tile phase stamps (s_memtime, shader cycles) of workgroup 0's waves, stored after the
+// per-workgroup area: [wave][tile < 64][6] = tile start, scores ready, softmax done, PV issued,
+// DMA landed, barrier passed
+__device__ __forceinline__ void phase_stamp(uint64_t* at) {
+  __builtin_amdgcn_sched_barrier(0);
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0) *at = t;
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 // value select (a ?: between two named variables is an lvalue: clang selects their ADDRESSES,
 // which keeps SROA from promoting them and sends them to scratch)
@@ -132,37 +148,48 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
   ECHO_INIT_SEG(2)
   ECHO_INIT_SEG(3)
 #undef ECHO_INIT_SEG
-  // segment of flat tile ti, each field selected as a scalar
-  auto pick = [&](int ti) -> SegInfo {
-    const int sg = ti >= fi3 && ke3 > 0 ? 3 : ti >= fi2 && ke2 > 0 ? 2 : ti >= fi1 && ke1 > 0 ? 1 : 0;
-#define ECHO_SEL(f) sel4(sg, f##0, f##1, f##2, f##3)
-    SegInfo d;
-    d.kb = ECHO_SEL(kb);
-    d.vb = ECHO_SEL(vb);
-    d.ld = ECHO_SEL(ld);
-    d.kend = ECHO_SEL(ke);
-    d.causal = ECHO_SEL(ca);
-    d.first = ECHO_SEL(fi);
-#undef ECHO_SEL
-    return d;
+  // Tile cursors over the flat tile list: scalar state advanced one tile per call (tiles are
+  // visited in order by each cursor), segment fields re-selected only when a segment ends.
+  struct Cursor {
+    int seg, left, t0, kend, causal, ld;
+    const bf16_t *kb, *vb;
   };
+  auto advance = [&](Cursor& c) __attribute__((always_inline)) {
+    if (c.left == 0) {
+      do { ++c.seg; } while (c.seg < 3 && sel4(c.seg, ke0, ke1, ke2, ke3) <= 0);
+      c.kb = sel4(c.seg, kb0, kb1, kb2, kb3);
+      c.vb = sel4(c.seg, vb0, vb1, vb2, vb3);
+      c.ld = (int)sel4(c.seg, ld0, ld1, ld2, ld3);
+      c.kend = sel4(c.seg, ke0, ke1, ke2, ke3);
+      c.causal = sel4(c.seg, ca0, ca1, ca2, ca3);
+      c.t0 = 0;
+      c.left = (c.kend + KTT - 1) / KTT;
+    } else {
+      c.t0 += KTT;
+    }
+    --c.left;
+  };
+  Cursor dmc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // DMA / load side
+  Cursor cpc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // compute side
 
-  // DMA of tile ti into buffer `buf`: 64 rows x 256 B for K and V = 32 wave-instructions
-  // of 1 KiB (4 rows each); lane-linear LDS image, XOR swizzle applied on the source chunk.
+  // DMA of the next tile (dmc) into buffer `buf`: 64 rows x 256 B for K and V = 32
+  // wave-instructions of 1 KiB (4 rows each); lane-linear LDS image, XOR swizzle applied on the
+  // source chunk; rows past the segment's valid length are clamped to its last row.
   const int dr = lane >> 4, dp = lane & 15;
-  auto dma_tile = [&](int ti, int buf) {
-    const SegInfo d = pick(ti);
-    const int t0 = (ti - d.first) * KTT;
+  auto dma_tile = [&](int buf) __attribute__((always_inline)) {
+    advance(dmc);
+    const int last = dmc.kend - 1 - dmc.t0;
+    const bf16_t* kbase = dmc.kb + (int64_t)dmc.t0 * dmc.ld;
+    const bf16_t* vbase = dmc.vb + (int64_t)dmc.t0 * dmc.ld;
 #pragma unroll
     for (int i = 0; i < DPT; ++i) {
       const int r = (i * NW + w) * 4 + dr;  // tile row 0..63 written by this lane
-      const int64_t tok = min(t0 + r, d.kend - 1);
-      const int c = dp ^ swz(r);
+      const uint32_t voff = (uint32_t)(min(r, last) * dmc.ld + ((dp ^ swz(r)) * 8)) * 2u;
       const int dst = ((i * NW + w) * 4) * 128;
       const uint32_t kdst = __builtin_amdgcn_readfirstlane(lds_addr_of(lds + (buf * 2) * KTT * 128 + dst));
       const uint32_t vdst = __builtin_amdgcn_readfirstlane(lds_addr_of(lds + (buf * 2 + 1) * KTT * 128 + dst));
-      glds16(d.kb + tok * d.ld + c * 8, kdst);
-      glds16(d.vb + tok * d.ld + c * 8, vdst);
+      glds16s(kbase, voff, kdst);
+      glds16s(vbase, voff, vdst);
     }
   };
 
@@ -177,15 +204,14 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
 
   // register staging: thread t moves 16-B chunks c = t + i*64*NW (row c>>4, chunk c&15) of K and V
   u32x4 kreg[DPT], vreg[DPT];
-  auto load_tile = [&](int ti) {
-    const SegInfo d = pick(ti);
-    const int t0 = (ti - d.first) * KTT;
+  auto load_tile = [&]() {
+    advance(dmc);
 #pragma unroll
     for (int i = 0; i < DPT; ++i) {
       const int c = tid + i * 64 * NW;
-      const int64_t tok = min(t0 + (c >> 4), d.kend - 1);
-      kreg[i] = *(const u32x4*)(d.kb + tok * d.ld + (c & 15) * 8);
-      vreg[i] = *(const u32x4*)(d.vb + tok * d.ld + (c & 15) * 8);
+      const int64_t tok = dmc.t0 + min(c >> 4, dmc.kend - 1 - dmc.t0);
+      kreg[i] = *(const u32x4*)(dmc.kb + tok * dmc.ld + (c & 15) * 8);
+      vreg[i] = *(const u32x4*)(dmc.vb + tok * dmc.ld + (c & 15) * 8);
     }
   };
   auto store_tile = [&](int buf) {
@@ -200,13 +226,13 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
   };
 
   if constexpr (ST == 0) {
-    if (ntiles > 0) { load_tile(0); store_tile(0); }
-    if (ntiles > 1) load_tile(1);
+    if (ntiles > 0) { load_tile(); store_tile(0); }
+    if (ntiles > 1) load_tile();
   } else {
     // prologue: tiles 0 .. ST-2 in flight, wait for tile 0
 #pragma unroll
     for (int p = 0; p < ST - 1; ++p)
-      if (p < ntiles) dma_tile(p, p);
+      if (p < ntiles) dma_tile(p);
     if (ST == 3 && ntiles > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPT) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -215,21 +241,22 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
   const uint64_t ts1 = (ABL & 128) ? rt_now() : 0;
   int cur = 0;
   if (ABL & 64) ntiles = 0;
+  uint64_t* ph = ((ABL & 512) && blockIdx.x == 0) ? g_attn_stamps + (int64_t)gridDim.x * 6 + w * 64 * 6 : nullptr;
   for (int ti = 0; ti < ntiles; ++ti) {
+    if ((ABL & 512) && ph && ti < 64) phase_stamp(ph + ti * 6 + 0);
     if constexpr (ST == 0) {
       // buffer cur^1 held tile ti-1: every wave passed the barrier after reading it
       if (ti + 1 < ntiles && !(ABL & 1)) store_tile(cur ^ 1);
-      if (ti + 2 < ntiles && !(ABL & 1)) load_tile(ti + 2);
+      if (ti + 2 < ntiles && !(ABL & 1)) load_tile();
     } else {
       // tile ti+ST-1 into the stage tile ti-1 used (all waves passed the barrier after reading it)
-      if (ti + ST - 1 < ntiles && !(ABL & 1)) dma_tile(ti + ST - 1, cur == 0 ? ST - 1 : cur - 1);
+      if (ti + ST - 1 < ntiles && !(ABL & 1)) dma_tile(cur == 0 ? ST - 1 : cur - 1);
     }
     const bf16_t* Ks = lds + (cur * 2) * KTT * 128;
     const bf16_t* Vs = Ks + KTT * 128;
-    const SegInfo d = pick(ti);
-    const int t0 = (ti - d.first) * KTT;
-    const int kend = d.kend;
-    const bool full = (t0 + KTT <= kend) && !d.causal;
+    advance(cpc);
+    const int t0 = cpc.t0, kend = cpc.kend;
+    const bool full = (t0 + KTT <= kend) && !cpc.causal;
 
     // ---- S^T = K . Q^T for two 32-key sub-tiles
     f32x16 st[NKK];
@@ -250,10 +277,25 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
         st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], st[kk], 0, 0, 0);
       }
     }
+    if (!(ABL & 8)) {
+      // K fragment reads run 4 MFMAs ahead (hipcc otherwise waits on each read right before its
+      // MFMA: 16 serialised LDS latencies, ≈2.7k cycles per tile measured with ablation 512)
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 2);
+#pragma unroll
+      for (int i = 0; i < 8 * NKK; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+        if (i + 4 < 8 * NKK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 2);
+      }
+    }
     if (ABL & 256) __builtin_amdgcn_s_setprio(0);
     // ---- mask (partial tiles only), online softmax (lane = query, registers = keys).
     // The running max is kept on RAW scores (scale > 0 preserves the argmax); one FMA per score
     // forms the exp2 argument s*c - m*c; raw v_exp_f32 (results < 2^-126 flush to 0).
+    if ((ABL & 512) && ph && ti < 64) {  // a VALU read of the last QK result waits for the MFMA chain
+      float dmy;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(dmy) : "v"(st[NKK - 1][15]));
+      phase_stamp(ph + ti * 6 + 1);
+    }
     float mx = -INFINITY;
     if (!(ABL & 2)) {
     if (!full) {
@@ -262,7 +304,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = t0 + kk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
-          const bool ok = key < kend && (!d.causal || key <= qi);
+          const bool ok = key < kend && (!cpc.causal || key <= qi);
           st[kk][r] = ok ? st[kk][r] : -INFINITY;
         }
     }
@@ -293,6 +335,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
     l_run += psum;
     m_run = m_new;
     }
+    if ((ABL & 512) && ph && ti < 64) phase_stamp(ph + ti * 6 + 2);
 
     if (ABL & 256) __builtin_amdgcn_s_setprio(1);
     // ---- O^T += V^T . P  (P from the accumulators, V^T by transposed LDS reads)
@@ -326,7 +369,17 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
           o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf, o[dt], 0, 0, 0);
         }
       }
+    if (!(ABL & 4) && !(ABL & 16)) {
+      // V^T transposed reads (2 per MFMA) run 2 MFMAs ahead
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 3);
+#pragma unroll
+      for (int i = 0; i < 8 * NKK; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 3);
+        if (i + 2 < 8 * NKK) __builtin_amdgcn_sched_group_barrier(0x100, 2, 3);
+      }
+    }
     if (ABL & 256) __builtin_amdgcn_s_setprio(0);
+    if ((ABL & 512) && ph && ti < 64) phase_stamp(ph + ti * 6 + 3);
     if constexpr (ST == 0) {
       __syncthreads();  // tile ti+1 was written at the top of this tile
       cur ^= 1;
@@ -334,7 +387,9 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
       // tile ti+1 landed (this wave's share; later tiles may stay in flight) ... and everyone's
       if (ST == 3 && ti + 2 < ntiles && !(ABL & 1)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPT) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if ((ABL & 512) && ph && ti < 64) phase_stamp(ph + ti * 6 + 4);
       __syncthreads();
+      if ((ABL & 512) && ph && ti < 64) phase_stamp(ph + ti * 6 + 5);
       cur = cur == ST - 1 ? 0 : cur + 1;
     }
   }
@@ -786,6 +841,8 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 64: ECHO_ATTN_LAUNCH(64, NW, ST); break;     \
     case 128: ECHO_ATTN_LAUNCH(128, NW, ST); break;   \
     case 256: ECHO_ATTN_LAUNCH(256, NW, ST); break;   \
+    case 640: ECHO_ATTN_LAUNCH(640, NW, ST); break;   \
+    case 641: ECHO_ATTN_LAUNCH(641, NW, ST); break;   \
     default: return ECHO_EINVAL;                      \
   }
   switch (cfg) {
@@ -829,8 +886,8 @@ extern "C" int echo_attention_variant(const EchoAttnArgs* a, int32_t variant, in
   const int rc = check_attn_args(a);
   if (rc) return rc;
   if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
-  if ((ablation & 128) && (!stamps || variant > 4)) return ECHO_EINVAL;  // stamps: attn_bf16_kernel variants
-  if (ablation & 128) {
+  if ((ablation & 640) && (!stamps || variant > 4)) return ECHO_EINVAL;  // stamps: attn_bf16_kernel variants
+  if (ablation & 640) {
     if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_attn_stamps), &stamps, sizeof(stamps), 0, hipMemcpyHostToDevice,
                                (hipStream_t)stream) != hipSuccess)
       return ECHO_EINVAL;

@@ -103,7 +103,9 @@ int echo_attention(const EchoAttnArgs* args, void* stream);
  * measurement variants of the bf16 attention kernel. variant 0 = the production kernel;
  * ablation != 0 removes parts of the work (results are then WRONG, timing only); ablation bit 128
  * records per-workgroup s_memrealtime stamps into `stamps` (device, [workgroups][6] uint64:
- * entry, prologue landed, tile loop done, exit, tiles, XCD). Variants/bits: csrc/attention.hip. */
+ * entry, prologue landed, tile loop done, exit, tiles, XCD); bit 512 (with 128) additionally
+ * records per-tile phase cycles of workgroup 0 after that area ([4 waves][64][6]).
+ * Variants/bits: csrc/attention.hip. */
 int echo_attention_variant(const EchoAttnArgs* args, int32_t variant, int32_t ablation, uint64_t* stamps,
                            void* stream);
 

@@ -6,8 +6,26 @@ import sys
 import numpy as np
 
 
+def phases(p):
+    """Per-tile phase cycles of workgroup 0 (ablation 512): [4 waves][64 tiles][6 stamps]."""
+    p = p.reshape(4, 64, 6).astype(np.int64)
+    names = ["QK issue+wait", "softmax", "PV issue", "DMA wait", "barrier"]
+    for w in range(4):
+        rows = p[w][p[w][:, 0] > 0]
+        if len(rows) < 2:
+            continue
+        d = np.diff(rows, axis=1)
+        per = np.diff(rows[:, 0])
+        print(f"wave {w}: {len(rows)} tiles, mean cycles/tile {per.mean():7.0f}  " +
+              "  ".join(f"{n} {d[:, i].mean():6.0f}" for i, n in enumerate(names)))
+
+
 def main():
     a = np.load(sys.argv[1]).reshape(-1, 6).astype(np.int64)
+    nwg = int(sys.argv[2]) if len(sys.argv) > 2 else len(a) - 256
+    if len(a) > nwg and a[nwg:].any():
+        phases(a[nwg:nwg + 256])
+    a = a[:nwg]
     t0 = a[:, 0].min()
     ent, pro, loop, ext = (a[:, i] - t0 for i in range(4))
     nt = a[:, 4]

@@ -55,14 +55,15 @@ def main():
                 fn = lambda: ops.attention(qkvg[:, :, 0], segs, out=out, gate=qkvg[:, :, 3])  # noqa: E731
             else:
                 nwg = ((N + 127) // 128) * H * R * 2  # upper bound over variants (QB >= 128)
-                st = torch.zeros((nwg, 6), device=dev, dtype=torch.int64) if args.ablation & 128 else None
+                n = ((N + 127) // 128) * H * R
+                st = (torch.zeros((n + 4 * 64, 6), device=dev, dtype=torch.int64)
+                      if args.ablation & 128 else None)
                 fn = lambda: ops.attention_variant(qkvg[:, :, 0], segs, out=out, gate=qkvg[:, :, 3],  # noqa: E731
                                                    variant=args.variant or 0, ablation=args.ablation, stamps=st)
             ms = timeit(fn)
             if args.stamps and args.ablation & 128:
                 import numpy as np
-                n = ((N + 127) // 128) * H * R
-                np.save(args.stamps, st[:n].cpu().numpy())
+                np.save(args.stamps, st.cpu().numpy())
             print(f"R={R:3d} {name:10s} {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TFLOP/s", flush=True)
 
 
