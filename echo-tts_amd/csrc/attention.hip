@@ -72,6 +72,59 @@ __device__ __forceinline__ T sel4(int sg, T a0, T a1, T a2, T a3) {
   return sg == 3 ? a3 : sg == 2 ? a2 : sg == 1 ? a1 : a0;
 }
 
+// ---- shared by the bf16 kernels: per-workgroup segment table and tile cursors.
+// Segment fields live in named scalars (struct copies / runtime-indexed arrays of them go to
+// scratch; kernel-argument references copy the whole argument block to scratch), filled straight
+// from the kernel arguments; needs a, row, head, q0, QB, KTT in scope.
+#define ECHO_SEG_TABLE()                                                                       \
+  const bf16_t *kb0 = nullptr, *kb1 = nullptr, *kb2 = nullptr, *kb3 = nullptr;                 \
+  const bf16_t *vb0 = nullptr, *vb1 = nullptr, *vb2 = nullptr, *vb3 = nullptr;                 \
+  int64_t ld0 = 0, ld1 = 0, ld2 = 0, ld3 = 0;                                                  \
+  int ke0 = 0, ke1 = 0, ke2 = 0, ke3 = 0, ca0 = 0, ca1 = 0, ca2 = 0, ca3 = 0;                  \
+  int ntiles = 0;                                                                              \
+  ECHO_SEG_ENTRY(0)                                                                            \
+  ECHO_SEG_ENTRY(1)                                                                            \
+  ECHO_SEG_ENTRY(2)                                                                            \
+  ECHO_SEG_ENTRY(3)
+#define ECHO_SEG_ENTRY(SG)                                                                     \
+  if (SG < a.nseg && a.seg[SG].k) {                                                            \
+    const int len_ = a.seg[SG].len ? a.seg[SG].len[row] : a.seg[SG].capacity;                  \
+    int kend_ = min(len_, a.seg[SG].capacity);                                                 \
+    if (a.seg[SG].causal) kend_ = min(kend_, q0 + QB);                                         \
+    kend_ = max(kend_, 0);                                                                     \
+    const int b_ = row % a.seg[SG].batch_mod;                                                  \
+    kb##SG = (const bf16_t*)a.seg[SG].k + b_ * a.seg[SG].ld_batch + head * 128;                \
+    vb##SG = (const bf16_t*)a.seg[SG].v + b_ * a.seg[SG].ld_batch + head * 128;                \
+    ld##SG = a.seg[SG].ld_tok;                                                                 \
+    ke##SG = kend_;                                                                            \
+    ca##SG = a.seg[SG].causal;                                                                 \
+    ntiles += (kend_ + KTT - 1) / KTT;                                                         \
+  }
+
+// Tile cursor over the flat tile list [segment 0 tiles | segment 1 tiles | ...]: scalar state
+// advanced one tile per call (each cursor visits tiles in order); segment fields are re-selected
+// only when a segment ends.
+struct Cursor {
+  int seg, left, t0, kend, causal, ld;
+  const bf16_t *kb, *vb;
+};
+#define ECHO_CURSOR_ADVANCE()                                                                  \
+  auto advance = [&](Cursor& c) __attribute__((always_inline)) {                               \
+    if (c.left == 0) {                                                                         \
+      do { ++c.seg; } while (c.seg < 3 && sel4(c.seg, ke0, ke1, ke2, ke3) <= 0);               \
+      c.kb = sel4(c.seg, kb0, kb1, kb2, kb3);                                                  \
+      c.vb = sel4(c.seg, vb0, vb1, vb2, vb3);                                                  \
+      c.ld = (int)sel4(c.seg, ld0, ld1, ld2, ld3);                                             \
+      c.kend = sel4(c.seg, ke0, ke1, ke2, ke3);                                                \
+      c.causal = sel4(c.seg, ca0, ca1, ca2, ca3);                                              \
+      c.t0 = 0;                                                                                \
+      c.left = (c.kend + KTT - 1) / KTT;                                                       \
+    } else {                                                                                   \
+      c.t0 += KTT;                                                                             \
+    }                                                                                          \
+    --c.left;                                                                                  \
+  };
+
 struct SegInfo {
   const bf16_t* kb;
   const bf16_t* vb;
@@ -121,54 +174,9 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
 
   // flat list of 64-key tiles over the (up to 4) segments; per-segment fields are kept in
   // named scalars (no runtime-indexed arrays: those go to scratch)
-  // per-segment fields as named scalars (struct copies / runtime-indexed arrays go to scratch)
-  const bf16_t *kb0 = nullptr, *kb1 = nullptr, *kb2 = nullptr, *kb3 = nullptr;
-  const bf16_t *vb0 = nullptr, *vb1 = nullptr, *vb2 = nullptr, *vb3 = nullptr;
-  int64_t ld0 = 0, ld1 = 0, ld2 = 0, ld3 = 0;
-  int ke0 = 0, ke1 = 0, ke2 = 0, ke3 = 0, ca0 = 0, ca1 = 0, ca2 = 0, ca3 = 0;
-  int fi0 = 0, fi1 = 0, fi2 = 0, fi3 = 0;
-  int ntiles = 0;
-#define ECHO_INIT_SEG(SG)                                                                  \
-  fi##SG = ntiles;                                                                         \
-  if (SG < a.nseg && a.seg[SG].k) {                                                        \
-    const int len = a.seg[SG].len ? a.seg[SG].len[row] : a.seg[SG].capacity;              \
-    int kend = min(len, a.seg[SG].capacity);                                               \
-    if (a.seg[SG].causal) kend = min(kend, q0 + QB);                                       \
-    kend = max(kend, 0);                                                                   \
-    const int b = row % a.seg[SG].batch_mod;                                               \
-    kb##SG = (const bf16_t*)a.seg[SG].k + b * a.seg[SG].ld_batch + head * 128;             \
-    vb##SG = (const bf16_t*)a.seg[SG].v + b * a.seg[SG].ld_batch + head * 128;             \
-    ld##SG = a.seg[SG].ld_tok;                                                             \
-    ke##SG = kend;                                                                         \
-    ca##SG = a.seg[SG].causal;                                                             \
-    ntiles += (kend + KTT - 1) / KTT;                                                        \
-  }
-  ECHO_INIT_SEG(0)
-  ECHO_INIT_SEG(1)
-  ECHO_INIT_SEG(2)
-  ECHO_INIT_SEG(3)
-#undef ECHO_INIT_SEG
-  // Tile cursors over the flat tile list: scalar state advanced one tile per call (tiles are
-  // visited in order by each cursor), segment fields re-selected only when a segment ends.
-  struct Cursor {
-    int seg, left, t0, kend, causal, ld;
-    const bf16_t *kb, *vb;
-  };
-  auto advance = [&](Cursor& c) __attribute__((always_inline)) {
-    if (c.left == 0) {
-      do { ++c.seg; } while (c.seg < 3 && sel4(c.seg, ke0, ke1, ke2, ke3) <= 0);
-      c.kb = sel4(c.seg, kb0, kb1, kb2, kb3);
-      c.vb = sel4(c.seg, vb0, vb1, vb2, vb3);
-      c.ld = (int)sel4(c.seg, ld0, ld1, ld2, ld3);
-      c.kend = sel4(c.seg, ke0, ke1, ke2, ke3);
-      c.causal = sel4(c.seg, ca0, ca1, ca2, ca3);
-      c.t0 = 0;
-      c.left = (c.kend + KTT - 1) / KTT;
-    } else {
-      c.t0 += KTT;
-    }
-    --c.left;
-  };
+  ECHO_SEG_TABLE()
+
+  ECHO_CURSOR_ADVANCE()
   Cursor dmc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // DMA / load side
   Cursor cpc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // compute side
 
@@ -437,28 +445,24 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
 
 // ----------------------------------------------------------------------------- software-pipelined
 // Same tile math, LDS image and numerics as attn_bf16_kernel<0,4,2>, scheduled so that every wave
-// overlaps its own MFMA and VALU work (cdna_hip_programming.md T15):
+// overlaps its own MFMA and VALU work (cdna_hip_programming.md T15), two workgroups per CU:
 //   phase A of iteration t: S(t+1) = K(t+1).Q^T (16 MFMA)  ||  softmax finish of tile t
 //                           (exp2, row sums, bf16 pack of P(t))
 //   phase B of iteration t: O^T += V(t)^T.P(t) (16 MFMA)   ||  row max of S(t+1)
 // K and V have separate double buffers: K(t+2) and V(t+1) are issued at the top of iteration t
 // (their slots held K(t) and V(t-1), both consumed in iteration t-1); one barrier per iteration.
-// sched_group_barrier pins the MFMA / LDS-read / VALU interleave (T19).
+// sched_group_barrier pins the MFMA / LDS-read / VALU interleave (T19), reads 2-4 MFMAs ahead.
 constexpr int SG_MFMA = 0x8, SG_VALU = 0x2, SG_DSR = 0x100, SG_TRANS = 0x400;
 
 template <int ABL>
-__global__ void __launch_bounds__(256, 1) attn_pipe_kernel(EchoAttnArgs a) {
-  constexpr int NW = 4, QB = 128, DPT = 4;
-  constexpr int NS = 3;  // ring slots per K and per V
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * NS * KT * 128];  // K slots | V slots
+__global__ void __launch_bounds__(256, 2) attn_pipe_kernel(EchoAttnArgs a) {
+  constexpr int NW = 4, QB = 128, DPT = 4, KTT = KT;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[4 * KT * 128];  // K slot 0, 1 | V slot 0, 1
 
   const int nqb = (a.n_q + QB - 1) / QB;
   const int L = remap_xcd(blockIdx.x, gridDim.x);
   const int qb = L % nqb;
-  // rows fastest: each XCD's contiguous block range then covers every row type (cond /
-  // uncond-text / uncond-speaker rows have different key counts), and the CFG rows that share
-  // one text/speaker K/V copy land on the same XCD
-  const int row = (L / nqb) % a.rows;
+  const int row = (L / nqb) % a.rows;  // rows fastest (see attn_bf16_kernel)
   const int head = L / (nqb * a.rows);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -474,73 +478,36 @@ __global__ void __launch_bounds__(256, 1) attn_pipe_kernel(EchoAttnArgs a) {
 #pragma unroll
   for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));
 
-  const bf16_t *kb0 = nullptr, *kb1 = nullptr, *kb2 = nullptr, *kb3 = nullptr;
-  const bf16_t *vb0 = nullptr, *vb1 = nullptr, *vb2 = nullptr, *vb3 = nullptr;
-  int64_t ld0 = 0, ld1 = 0, ld2 = 0, ld3 = 0;
-  int ke0 = 0, ke1 = 0, ke2 = 0, ke3 = 0, ca0 = 0, ca1 = 0, ca2 = 0, ca3 = 0;
-  int fi0 = 0, fi1 = 0, fi2 = 0, fi3 = 0;
-  int ntiles = 0;
-#define ECHO_INIT_SEG(SG)                                                                  \
-  fi##SG = ntiles;                                                                         \
-  if (SG < a.nseg && a.seg[SG].k) {                                                        \
-    const int len = a.seg[SG].len ? a.seg[SG].len[row] : a.seg[SG].capacity;              \
-    int kend = min(len, a.seg[SG].capacity);                                               \
-    if (a.seg[SG].causal) kend = min(kend, q0 + QB);                                       \
-    kend = max(kend, 0);                                                                   \
-    const int b = row % a.seg[SG].batch_mod;                                               \
-    kb##SG = (const bf16_t*)a.seg[SG].k + b * a.seg[SG].ld_batch + head * 128;             \
-    vb##SG = (const bf16_t*)a.seg[SG].v + b * a.seg[SG].ld_batch + head * 128;             \
-    ld##SG = a.seg[SG].ld_tok;                                                             \
-    ke##SG = kend;                                                                         \
-    ca##SG = a.seg[SG].causal;                                                             \
-    ntiles += (kend + KT - 1) / KT;                                                        \
-  }
-  ECHO_INIT_SEG(0)
-  ECHO_INIT_SEG(1)
-  ECHO_INIT_SEG(2)
-  ECHO_INIT_SEG(3)
-#undef ECHO_INIT_SEG
-  auto pick = [&](int ti) __attribute__((always_inline)) -> SegInfo {
-    const int sg = ti >= fi3 && ke3 > 0 ? 3 : ti >= fi2 && ke2 > 0 ? 2 : ti >= fi1 && ke1 > 0 ? 1 : 0;
-#define ECHO_SEL(f) sel4(sg, f##0, f##1, f##2, f##3)
-    SegInfo d;
-    d.kb = ECHO_SEL(kb);
-    d.vb = ECHO_SEL(vb);
-    d.ld = ECHO_SEL(ld);
-    d.kend = ECHO_SEL(ke);
-    d.causal = ECHO_SEL(ca);
-    d.first = ECHO_SEL(fi);
-#undef ECHO_SEL
-    return d;
-  };
+  ECHO_SEG_TABLE()
+  ECHO_CURSOR_ADVANCE()
+  Cursor kc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // K DMA (two tiles ahead of compute)
+  Cursor vc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // V DMA (one tile ahead)
+  Cursor mc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // masking of the tile whose scores are formed
 
-  // K (part 0) or V (part 1) of tile ti into its slot: 64 rows x 256 B = 16 wave-instructions
+  // K (part 0) or V (part 1) of the cursor's next tile into `slot` (16 wave-instructions of 1 KiB)
   const int dr = lane >> 4, dp = lane & 15;
-  auto dma_part = [&](int ti, int part) __attribute__((always_inline)) {
-    const SegInfo d = pick(ti);
-    const int t0 = (ti - d.first) * KT;
-    const bf16_t* base = part ? d.vb : d.kb;
-    const bf16_t* slot = lds + (part * NS + ti % NS) * KT * 128;
+  auto dma_part = [&](Cursor& c, int part, int slot) __attribute__((always_inline)) {
+    advance(c);
+    const int last = c.kend - 1 - c.t0;
+    const bf16_t* base = (part ? c.vb : c.kb) + (int64_t)c.t0 * c.ld;
 #pragma unroll
     for (int i = 0; i < DPT; ++i) {
       const int r = (i * NW + w) * 4 + dr;
-      const int64_t tok = min(t0 + r, d.kend - 1);
-      const int c = dp ^ swz(r);
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr_of(slot + ((i * NW + w) * 4) * 128));
-      glds16(base + tok * d.ld + c * 8, dst);
+      const uint32_t voff = (uint32_t)(min(r, last) * c.ld + ((dp ^ swz(r)) * 8)) * 2u;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          lds_addr_of(lds + (part * 2 + slot) * KT * 128 + ((i * NW + w) * 4) * 128));
+      glds16s(base, voff, dst);
     }
   };
-  // -inf for keys past the segment's valid length (and above the diagonal when causal)
-  auto mask_tile = [&](int ti, f32x16 (&st)[2]) __attribute__((always_inline)) {
-    const SegInfo d = pick(ti);
-    const int t0 = (ti - d.first) * KT;
-    if (t0 + KT <= d.kend && !d.causal) return;
+  auto mask_tile = [&](f32x16 (&st)[2]) __attribute__((always_inline)) {
+    advance(mc);
+    if (mc.t0 + KT <= mc.kend && !mc.causal) return;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int key = t0 + kk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
-        const bool ok = key < d.kend && (!d.causal || key <= qi);
+        const int key = mc.t0 + kk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
+        const bool ok = key < mc.kend && (!mc.causal || key <= qi);
         st[kk][r] = ok ? st[kk][r] : -INFINITY;
       }
   };
@@ -582,15 +549,12 @@ __global__ void __launch_bounds__(256, 1) attn_pipe_kernel(EchoAttnArgs a) {
   // iteration t: sc = raw scores of tile t (masked), mxc = their row max; produces sn / mxn for t+1
   auto iter = [&](int t, f32x16 (&sc)[2], float mxc, f32x16 (&sn)[2], float& mxn) __attribute__((always_inline)) {
     const bool has_next = t + 1 < ntiles;
-    // K(t+3) into the slot of K(t) (consumed by QK(t) in iteration t-1), V(t+2) into the slot of
-    // V(t-1) (consumed by PV(t-1)); both waited for two iterations later
-    const int nk = t + 3 < ntiles, nv = t + 2 < ntiles;
     if (!(ABL & 1)) {
-      if (nk) dma_part(t + 3, 0);
-      if (nv) dma_part(t + 2, 1);
+      if (t + 2 < ntiles) dma_part(kc, 0, t & 1);   // K(t+2) into the slot of K(t)
+      if (has_next) dma_part(vc, 1, (t + 1) & 1);    // V(t+1) into the slot of V(t-1)
     }
-    const bf16_t* Kn = lds + ((t + 1) % NS) * KT * 128;
-    const bf16_t* Vc = lds + (NS + t % NS) * KT * 128;
+    const bf16_t* Kn = lds + ((t + 1) & 1) * KT * 128;
+    const bf16_t* Vc = lds + (2 + (t & 1)) * KT * 128;
     const float m_new = fmaxf(m_run, mxc);
     const float msc = m_new == -INFINITY ? 0.f : -m_new * sl2;
     if (__any(m_new != m_run)) {  // otherwise alpha == 1 exactly for every lane
@@ -621,13 +585,13 @@ __global__ void __launch_bounds__(256, 1) attn_pipe_kernel(EchoAttnArgs a) {
     if (has_next) {
       qk_tile(Kn, sn);
       softmax_finish();
-      // K fragment reads run 2 MFMAs ahead; per MFMA gap 2 exp + 3 other VALU (MI355X_MICROARCH
+      // K fragment reads 4 MFMAs ahead; per MFMA gap 2 exp + 3 other VALU (MI355X_MICROARCH
       // 'vector-instruction ISSUE cost': 2x8 + 3x4 + the MFMA's 8 stays near the 32-cycle gap)
-      __builtin_amdgcn_sched_group_barrier(SG_DSR, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_DSR, 4, 0);
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
-        if (k < 14) __builtin_amdgcn_sched_group_barrier(SG_DSR, 1, 0);
+        if (k < 12) __builtin_amdgcn_sched_group_barrier(SG_DSR, 1, 0);
         __builtin_amdgcn_sched_group_barrier(SG_TRANS, 2, 0);
         __builtin_amdgcn_sched_group_barrier(SG_VALU, 3, 0);
       }
@@ -636,8 +600,8 @@ __global__ void __launch_bounds__(256, 1) attn_pipe_kernel(EchoAttnArgs a) {
     }
     l_run += ps0 + ps1;
 
-    // ---- phase B: PV(t) || row max of S(t+1)
-    if (has_next) mask_tile(t + 1, sn);
+    // ---- phase B: PV(t) || row max of S(t+1) (garbage and unused when there is no t+1)
+    if (has_next) mask_tile(sn);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -657,8 +621,8 @@ __global__ void __launch_bounds__(256, 1) attn_pipe_kernel(EchoAttnArgs a) {
                                                            0, 0, 0);
         }
       }
-    if (has_next) mxn = row_max(sn);
-    // V^T transposed reads run 2 MFMAs ahead (2 per MFMA); the row max fills the gaps
+    mxn = row_max(sn);
+    // V^T transposed reads (2 per MFMA) 2 MFMAs ahead; the row max fills the gaps
     __builtin_amdgcn_sched_group_barrier(SG_DSR, 4, 1);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -666,30 +630,25 @@ __global__ void __launch_bounds__(256, 1) attn_pipe_kernel(EchoAttnArgs a) {
       if (k < 14) __builtin_amdgcn_sched_group_barrier(SG_DSR, 2, 1);
       __builtin_amdgcn_sched_group_barrier(SG_VALU, 2, 1);
     }
-    // K(t+2) and V(t+1) landed (this wave's share; this iteration's DMA may stay in flight)
-    // ... and everyone's; the slots of K(t+1) and V(t) are free after the barrier
-    if (nk && nv && !(ABL & 1)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPT) : "memory");
-    else if ((nk || nv) && !(ABL & 1)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPT) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // K(t+2) and V(t+1) landed (this wave's share) ... and everyone's; slots of K(t+1)/V(t) free
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
 
   f32x16 sa[2], sb[2];
   float mxa = -INFINITY, mxb = -INFINITY;
-  // prologue: K0 V0 K1 needed before iteration 0; V1 K2 stay in flight
-  if (ntiles > 0) { dma_part(0, 0); dma_part(0, 1); }
-  if (ntiles > 1) { dma_part(1, 0); dma_part(1, 1); }
-  if (ntiles > 2) dma_part(2, 0);
-  if (ntiles > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPT) : "memory");
-  else if (ntiles > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPT) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // prologue: K0 V0 K1; QK(0) and its row max; then K slot 0 is refilled (tile 2) in iteration 0
+  if (ntiles > 0) { dma_part(kc, 0, 0); dma_part(vc, 1, 0); }
+  if (ntiles > 1) dma_part(kc, 0, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (ntiles > 0) {
     qk_tile(lds, sa);
-    mask_tile(0, sa);
+    mask_tile(sa);
     mxa = row_max(sa);
   }
-  __syncthreads();  // K slot 0 is refilled (tile 3) at the top of iteration 0
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int t = 0; t < ntiles; t += 2) {
     iter(t, sa, mxa, sb, mxb);
     if (t + 1 >= ntiles) break;
@@ -704,8 +663,6 @@ __global__ void __launch_bounds__(256, 1) attn_pipe_kernel(EchoAttnArgs a) {
   bf16_t* op = (bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qi * a.o_ld_tok + head * 128;
   const bf16_t* gp = a.gate ? (const bf16_t*)a.gate + row * a.g_ld_batch + (int64_t)qi * a.g_ld_tok + head * 128
                             : nullptr;
-  // all 16 gate loads first: gate and out may alias as far as the compiler knows, so loads
-  // interleaved with the stores would serialise 16 memory latencies (≈10 us per workgroup)
   uint2 gg[16];
   if (gp) {
 #pragma unroll
@@ -818,10 +775,10 @@ int attn_grid(const EchoAttnArgs* a, int qb) { return ((a->n_q + qb - 1) / qb) *
 
 // Measurement variants of the bf16 kernel (tools/bench_attn.py; DESIGN.md §7 lists what each
 // showed). variant: 0 production (4 waves, 2-slot LDS-DMA ring, 64-key tiles), 1/2 8 waves with
-// a 2/3-slot ring, 3/4 register-staged K/V with 4/8 waves, 5 software-pipelined one-wave-per-SIMD
-// kernel, 6/7 32-key tiles with a 2/3-slot ring. ablation: the ABL bits of attn_bf16_kernel.
+// a 2/3-slot ring, 3/4 register-staged K/V with 4/8 waves, 5 software-pipelined kernel (two waves
+// per SIMD), 6/7 32-key tiles with a 2/3-slot ring. ablation: the ABL bits of attn_bf16_kernel.
 int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) {
-  const int qb = (cfg == 0 || cfg == 3 || cfg == 5 || cfg == 6 || cfg == 7) ? 128 : 256;
+  const int qb = (cfg == 1 || cfg == 2 || cfg == 4) ? 256 : 128;
   const dim3 grid(attn_grid(a, qb));
 #define ECHO_ATTN_LAUNCH(A, NW, ST, ...) hipLaunchKernelGGL((attn_bf16_kernel<A, NW, ST, ##__VA_ARGS__>), grid, dim3(64 * NW), 0, s, *a)
 #define ECHO_ATTN_ABLS(NW, ST)                        \
@@ -852,8 +809,8 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 3: ECHO_ATTN_ABLS(4, 0); break;
     case 4: ECHO_ATTN_ABLS(8, 0); break;
     case 5:
-      if (abl == 1) hipLaunchKernelGGL(attn_pipe_kernel<1>, grid, dim3(256), 0, s, *a);
-      else if (abl == 0) hipLaunchKernelGGL(attn_pipe_kernel<0>, grid, dim3(256), 0, s, *a);
+      if (abl == 1) hipLaunchKernelGGL((attn_pipe_kernel<1>), grid, dim3(256), 0, s, *a);
+      else if (abl == 0) hipLaunchKernelGGL((attn_pipe_kernel<0>), grid, dim3(256), 0, s, *a);
       else return ECHO_EINVAL;
       break;
     case 6: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 2, 32); break;

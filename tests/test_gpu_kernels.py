@@ -227,6 +227,27 @@ def test_attention_variants_match_production(variant):
         assert (st[:n, 3] >= st[:n, 0]).all() and (st[:n, 0] > 0).all()
 
 
+@pytest.mark.parametrize("variant", [5])
+@pytest.mark.parametrize("n", [1, 63, 200, 333])
+def test_attention_variant_causal_segments(variant, n):
+    """Pipelined variant on the blockwise layout: causal latent segment (odd lengths, partial
+    tiles, single-tile rows), a prefix segment with per-row lengths incl. 0, and a speaker segment."""
+    B, H = 2, 2
+    R = 3 * B
+    qkvg = torch.randn(R, n, 4, H, 128, device=DEV).to(BF)
+    kt = torch.randn(B, 96, 2, H, 128, device=DEV).to(BF)
+    ks = torch.randn(B, 130, 2, H, 128, device=DEV).to(BF)
+    tl = torch.tensor([50, 96, 0, 0, 1, 71], dtype=torch.int32, device=DEV)
+    segs = [ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=B),
+            ops.Segment(ks[:, :, 0], ks[:, :, 1], batch_mod=B),
+            ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2], causal=True)]
+    ref = torch.empty(R, n, H, 128, device=DEV, dtype=BF)
+    ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
+    got = torch.empty_like(ref)
+    ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=variant)
+    close_bf16(got, ref.float().cpu())
+
+
 @pytest.mark.parametrize("dtype", [BF, torch.float32])
 def test_attention_segments(dtype):
     B, N, H = 2, 200, 4
