@@ -55,6 +55,7 @@ class StepArgs(C.Structure):
 SIGNATURES = {
     "echo_gemm": (i32, [C.POINTER(GemmArgs), vp]),
     "echo_gemm_pick_tile": (i32, [i32, i32, i32, i32]),
+    "echo_gemm_set_diag": (i32, [i32, i32]),
     "echo_attention": (i32, [C.POINTER(AttnArgs), vp]),
     "echo_attention_variant": (i32, [C.POINTER(AttnArgs), i32, i32, vp, vp]),
     "echo_rmsnorm": (i32, [i32, vp, i64, vp, vp, i64, i32, i32, f32, vp]),

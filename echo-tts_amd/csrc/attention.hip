@@ -28,27 +28,6 @@ __device__ __forceinline__ int remap_xcd(int bid, int nwg) {
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 }
 
-// LDS-DMA (global_load_lds_dwordx4) issued through inline asm: hipcc does not see it, so it
-// cannot insert a conservative vmcnt(0) in front of the ds_reads of the OTHER buffer (it did
-// for the V transposed reads). Completion is waited for explicitly (vmcnt(0) + barrier at the
-// end of each tile). M0 is saved/restored inside the statement (cdna_hip_programming.md §5.7).
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(gsrc), "s"(lds_addr) : "memory");
-}
-
-// SADDR form: address = 64-bit scalar base + 32-bit per-lane byte offset (no 64-bit VALU math)
-__device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32_t lds_addr) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_addr) : "memory");
-}
-
-__device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
 constexpr int KT = 64;   // keys per tile
 
 // Diagnostics only (echo_attention_variant ablation bit 128, tools/attn_timeline.py): s_memrealtime

@@ -75,6 +75,22 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// LDS-DMA (global_load_lds_dwordx4) through inline asm, SADDR form: global address = 64-bit
+// scalar base + 32-bit per-lane byte offset, LDS destination = M0 (+ lane * 16). hipcc does not
+// see the DMA, so it inserts no conservative vmcnt(0) in front of LDS reads of the other buffer;
+// the caller waits for completion explicitly (s_waitcnt vmcnt). Compiler-inserted waits for
+// other vector-memory ops can only over-count younger operations, never under-wait. M0 is
+// saved/restored inside the statement (cdna_hip_programming.md §5.7).
+__device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_addr) : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 #define ECHO_LAUNCH_CHECK()                         \
   do {                                              \
     hipError_t _e = hipGetLastError();              \

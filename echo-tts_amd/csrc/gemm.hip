@@ -32,6 +32,7 @@ struct Epi {
   // ECHO_EPI_HEADNORM
   const void* hn_w; int64_t hn_w_stride; const float* hn_rope;
   int hn_heads, hn_nblk, hn_rope_heads, hn_seq_len, hn_pos0, hn_pos_mult; float hn_eps;
+  int stagger;  // diagnostic (tile 14): first-round start delay per CU group, 10 ns ticks
 };
 
 __device__ __forceinline__ float epi_pointwise(float v, const Epi& ep) {
@@ -163,7 +164,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
     // the long-latency loads overlap; in-place residual (aux == C) is safe because every
     // element is read and written by the same lane.
     constexpr int CHc = (EK == EK_SWIGLU ? TN / 2 : TN) / 8, RPIc = 64 / CHc, NIT = TM / RPIc;
-    constexpr int NB = NIT <= 16 ? NIT : 8;  // row chunks in flight per batch (register budget)
+    constexpr int NB = (EK == EK_RESID || NIT > 16) ? (NIT < 8 ? NIT : 8) : NIT;  // row chunks per batch (registers)
     const int c = lane % CHc;
     const int n = nbase + c * 8;
     if (n >= Nout) return;
@@ -580,6 +581,13 @@ gemm_bf16_pp2_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   for (int c = 0; c < 4; ++c) dma(c, 0);
   if (nk > 1) {
     dma(0, 1); dma(1, 1); dma(2, 1);
+    if (ep.stagger > 0 && bid < 256) {
+      // diagnostic: first-round workgroups start in 8 groups per XCD, `stagger` ticks apart, so
+      // the tile rounds (and their epilogue store bursts) are spread in time
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      const uint64_t until = t0 + (uint64_t)(((bid >> 3) & 7) * ep.stagger);
+      while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(2);
+    }
     vm_wait_n<8>();
   } else {
     vm_wait_n<2>();
@@ -636,7 +644,270 @@ gemm_bf16_pp2_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   if (wm == 0) pp_barrier();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (ep.epi == 99) {  // diagnostic (tile 15): no epilogue, accumulators kept live
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   gemm_epilogue<TM, TN, FM, FN, EK>(acc, lds, wid, wm, wn, lane, m0, n0, M, N, z, Cv, ldc, sC, ep);
+}
+
+// ----------------------------------------------------------------------------- persistent 2-phase
+// gemm_bf16_pp2_kernel's K loop (same LDS image, chunking and K order: bitwise-equal results) run
+// by one persistent workgroup per CU over tiles blockIdx.x, +gridDim.x, ... The epilogue works
+// from the accumulator registers (8-B row segments, no LDS staging) and runs AFTER the next
+// tile's prologue DMA has been issued, so the output store burst overlaps the next tile's first
+// loads instead of serialising with a workgroup teardown + relaunch.
+//   * vmcnt counts loads, stores and LDS-DMA in issue order: the SN epilogue stores of a wave are
+//     younger than the next tile's prologue DMA, so the waits of that prologue and of K-tile 0
+//     allow SN more operations in flight; the first wait of K-tile 1 retires them.
+//   * every wave issues exactly SN stores per tile (raw buffer stores; rows past M fall beyond the
+//     buffer's num_records and are dropped by the hardware), so the counted waits hold for any M.
+//   * RESID reads the residual + gate of the current tile BEFORE issuing the prologue DMA, and
+//     waits for them with vmcnt(14) (the 14 prologue DMA stay in flight).
+//   * measured: the stores must be acknowledged before K-tile 1's first wait, and
+//     with every CU storing its 128 KB tile at once that costs more than the relaunch it saves.
+constexpr int reg_epi_stores(int ek) { return ek == EK_SWIGLU ? 8 : 16; }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+template <int EK, int CP = 0>  // CP: cache policy bits of the epilogue stores (2 = nt; diagnostic)
+__global__ void __launch_bounds__(512)
+gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
+                    const bf16_t* __restrict__ W, int64_t ldw, int64_t sW,
+                    void* __restrict__ Cv, int64_t ldc, int64_t sC,
+                    int M, int N, int K, int tiles_m, int tiles_n, Epi ep) {
+  static_assert(EK == EK_STORE || EK == EK_SWIGLU || EK == EK_RESID, "register epilogue kinds");
+  constexpr int BM = 256, BN = 256, TM = 128, TN = 64, FM = 8, FN = 4;
+  constexpr int STAGE = (BM + BN) * BK;
+  constexpr int SN = reg_epi_stores(EK);
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int z = blockIdx.y;
+  A += z * sA;
+  W += z * sW;
+  const int ntl = tiles_m * tiles_n;
+  const int q8 = ntl >> 3, r8 = ntl & 7;
+  constexpr int GM = 8;
+  // tile t -> origin: gemm_bf16_pp2_kernel's XCD-chunked group-M order with t in place of the
+  // block id (t = blockIdx.x + r * gridDim.x keeps t & 7 = the XCD when gridDim.x % 8 == 0)
+  auto origin = [&](int t, int& m0, int& n0) __attribute__((always_inline)) {
+    const int xcd = t & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (t >> 3);
+    const int grp = wg / (GM * tiles_n);
+    const int fm = grp * GM;
+    const int gm = min(tiles_m - fm, GM);
+    const int rem = wg - grp * GM * tiles_n;
+    m0 = (fm + rem % gm) * BM;
+    n0 = (rem / gm) * BN;
+  };
+
+  // per-lane 32-bit byte offsets of the staging rows (SADDR-form DMA: half the VGPRs of pointers)
+  uint32_t doff[4][2];
+  auto setup = [&](int m0, int n0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = chunk_row(c, 2 * wid + h) + (lane >> 3);
+        const int gc = (lane & 7) ^ ((row >> 1) & 7);
+        const bool isA = (c == 0 || c == 3);
+        const int64_t e = isA ? (int64_t)min(m0 + row, M - 1) * lda : (int64_t)min(n0 + row, N - 1) * ldw;
+        doff[c][h] = (uint32_t)((e + gc * 8) * 2);
+      }
+  };
+  const uint32_t lds0 = lds_addr_of(lds);
+  auto dma = [&](int c, int kt) __attribute__((always_inline)) {
+    const bf16_t* base = ((c == 0 || c == 3) ? A : W) + kt * BK;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int rb = chunk_row(c, 2 * wid + h);
+      const uint32_t dst = lds0 + (uint32_t)(((kt & 1) * STAGE + ((c == 0 || c == 3) ? 0 : BM * BK) + rb * BK) * 2);
+      glds16s(base, doff[c][h], __builtin_amdgcn_readfirstlane(dst));
+    }
+  };
+  // tile prologue: K-tile 0 whole, chunks 0-2 of K-tile 1 (14 DMA per wave; the host ensures nk >= 2)
+  auto prologue = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dma(c, 0);
+    dma(0, 1); dma(1, 1); dma(2, 1);
+  };
+
+  const int nk = K / BK;
+  int t = blockIdx.x;
+  if (t >= ntl) return;
+  int m0, n0;
+  origin(t, m0, n0);
+  setup(m0, n0);
+  prologue();
+
+  const __amdgpu_buffer_rsrc_t crs = brsrc((bf16_t*)Cv + z * sC, (uint32_t)(((int64_t)(M - 1) * ldc + N) * 2));
+  const int frow = lane & 15;
+  const int fsw = frow >> 1;
+  const int cq = 4 * (lane >> 4);
+  bool first = true;
+  for (;;) {
+    if (first) vm_wait_n<8>(); else vm_wait_n<8 + SN>();
+    pp_barrier();
+    if (wm == 1) pp_barrier();  // waves 4-7 run one barrier (one segment) behind
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 af[4][2], bfr[4][2];
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16_t* As = lds + (kt & 1) * STAGE;
+      const bf16_t* Bs = As + BM * BK;
+      const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+      const bool xs = !first && kt == 0;  // the previous tile's SN stores are still counted
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            af[i][s] = *(const bf16x8*)(As + (wm * TM + ph * 64 + i * 16 + frow) * BK +
+                                        (((4 * s + (lane >> 4)) ^ fsw) * 8));
+        if (ph == 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              bfr[j][s] = *(const bf16x8*)(Bs + (wn * TN + j * 16 + frow) * BK +
+                                           (((4 * s + (lane >> 4)) ^ fsw) * 8));
+          if (n1) dma(3, kt + 1);
+          if (!n1) vm_wait_n<0>();
+          else if (xs) vm_wait_n<8 + SN>();
+          else vm_wait_n<8>();
+        } else {
+          if (n2) { dma(0, kt + 2); dma(1, kt + 2); dma(2, kt + 2); }
+          if (n2) { if (xs) vm_wait_n<8 + SN>(); else vm_wait_n<8>(); }
+          else if (n1) { if (xs) vm_wait_n<2 + SN>(); else vm_wait_n<2>(); }
+          else vm_wait_n<0>();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pp_barrier();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              acc[ph * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][s], af[i][s], acc[ph * 4 + i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        pp_barrier();
+      }
+    }
+    if (wm == 0) pp_barrier();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's last fragment reads are done: both LDS buffers are free
+
+    const int tnext = t + gridDim.x;
+    const bool more = tnext < ntl;
+    // Output layout after one v_permlane16_swap per packed word of a fragment pair (j0, j1) =
+    // (2p, 2p+1): lane group g = lane>>4 holds 8 consecutive columns of row m, at column
+    // p*32 + (g&1)*16 + (g>>1)*8 of the wave's 64 — 16-B stores, 64 B per row per instruction.
+    // N % 256 == 0 (host): no column overhang; rows >= M give byte offsets >= num_records
+    // (m*ld >= (M-1)*ld + N), which the buffer unit drops (stores) or reads as 0 (loads).
+    const int mb = m0 + wm * TM + (lane & 15);
+    const int g4 = lane >> 4;
+    const int cpos = (g4 & 1) * 16 + (g4 >> 1) * 8;   // column of this lane's 8 within a 32-column pair
+    const int nb = n0 + wn * TN + cpos;
+    auto swap_pair = [&](uint2 lo, uint2 hi) __attribute__((always_inline)) -> u32x4 {
+      const auto s0 = __builtin_amdgcn_permlane16_swap(lo.x, hi.x, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(lo.y, hi.y, false, false);
+      return u32x4{s0[0], s1[0], s0[1], s1[1]};
+    };
+    u32x4 xr[FM][FN / 2];
+    float g[FN / 2][8];
+    if constexpr (EK == EK_RESID) {
+      const __amdgpu_buffer_rsrc_t ars =
+          brsrc((const bf16_t*)ep.aux + z * ep.stride_aux, (uint32_t)(((int64_t)(M - 1) * ep.ld_aux + N) * 2));
+#pragma unroll
+      for (int ii = 0; ii < FM; ++ii) {
+        const uint32_t off = (uint32_t)(((mb + ii * 16) * ep.ld_aux + nb) * 2);
+#pragma unroll
+        for (int p = 0; p < FN / 2; ++p)
+          xr[ii][p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ars, off + p * 64, 0, 0));
+      }
+      if (ep.gate) {
+        const bf16_t* gp = (const bf16_t*)ep.gate + z * ep.stride_gate + nb;
+#pragma unroll
+        for (int p = 0; p < FN / 2; ++p) load8(gp + p * 32, g[p]);
+      }
+    }
+    int m0n = 0, n0n = 0;
+    if (more) {
+      origin(tnext, m0n, n0n);
+      setup(m0n, n0n);
+      prologue();
+    }
+    if constexpr (EK == EK_RESID) {
+      if (more) vm_wait_n<14>(); else vm_wait_n<0>();
+    }
+
+    // ---- epilogue from registers: exactly SN buffer stores per wave
+    if constexpr (EK == EK_SWIGLU) {
+      // gate/up column blocks interleaved by 16 (j = 2jj gate, 2jj+1 up), as gemm_epilogue; the
+      // two output fragments (jj = 0, 1) form the swapped pair: 8 columns of 32 per lane
+      const int nbo = n0 / 2 + wn * (TN / 2) + cpos;
+#pragma unroll
+      for (int ii = 0; ii < FM; ++ii) {
+        uint2 q[2];
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          float u[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float a = rbf(acc[ii][2 * jj][r]), b = rbf(acc[ii][2 * jj + 1][r]);
+            u[r] = rbf(silu_hw(a)) * b;
+          }
+          q[jj] = make_uint2(pack2bf(u[0], u[1]), pack2bf(u[2], u[3]));
+        }
+        const u32x4 o = swap_pair(q[0], q[1]);
+        __builtin_amdgcn_raw_buffer_store_b128(o, crs, (uint32_t)(((mb + ii * 16) * ldc + nbo) * 2), 0, CP);
+      }
+    } else {
+#pragma unroll
+      for (int ii = 0; ii < FM; ++ii) {
+        const uint32_t off = (uint32_t)(((mb + ii * 16) * ldc + nb) * 2);
+#pragma unroll
+        for (int p = 0; p < FN / 2; ++p) {
+          const f32x4& c0 = acc[ii][2 * p];
+          const f32x4& c1 = acc[ii][2 * p + 1];
+          u32x4 o = swap_pair(make_uint2(pack2bf(c0[0], c0[1]), pack2bf(c0[2], c0[3])),
+                              make_uint2(pack2bf(c1[0], c1[1]), pack2bf(c1[2], c1[3])));
+          if constexpr (EK == EK_RESID) {
+            // out = bf16(x + bf16(g * bf16(acc))): gemm_epilogue's stage-2 rounding points
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+              float v0 = bf2f(o[w] & 0xffffu), v1 = bf2f(o[w] >> 16);
+              if (ep.gate) { v0 = rbf(g[p][2 * w] * v0); v1 = rbf(g[p][2 * w + 1] * v1); }
+              v0 = bf2f(xr[ii][p][w] & 0xffffu) + v0;
+              v1 = bf2f(xr[ii][p][w] >> 16) + v1;
+              o[w] = pack2bf(v0, v1);
+            }
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(o, crs, off + p * 64, 0, CP);
+        }
+      }
+    }
+    if (!more) break;
+    t = tnext;
+    m0 = m0n;
+    n0 = n0n;
+    first = false;
+  }
 }
 
 // ----------------------------------------------------------------------------- fp32 (parity mode)
@@ -784,6 +1055,27 @@ int launch_pp2_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   return 0;
 }
 
+int g_num_cus = 0;  // persistent grid size (hipDeviceProp multiProcessorCount, queried once)
+
+template <int EK, int CP = 0>
+int launch_ps_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
+  const int tm = (a->M + 255) / 256, tn = (a->N + 255) / 256;
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return (int)e;
+    if (n <= 0) return ECHO_EINVAL;
+    g_num_cus = n;
+  }
+  const int grid = min(tm * tn, g_num_cus);
+  hipLaunchKernelGGL((gemm_bf16_ps_kernel<EK, CP>), dim3(grid, a->batch), dim3(512), 0, s, (const bf16_t*)a->A,
+                     a->lda, a->stride_a, (const bf16_t*)a->W, a->ldw, a->stride_w, a->C, a->ldc, a->stride_c,
+                     a->M, a->N, a->K, tm, tn, ep);
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
 // epilogue kind of a call: the specialised kinds need no bias, no activation and no divisor
 int ek_of(const EchoGemmArgs* a) {
   if (a->bias || a->act != ECHO_ACT_NONE || a->out_div != 0.0f) return EK_GENERIC;
@@ -803,6 +1095,27 @@ int launch_bf16(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
     case EK_SWIGLU: return launch_bf16_ek<BM, BN, WM, WN, EK_SWIGLU>(a, ep, s);
     case EK_RESID: return launch_bf16_ek<BM, BN, WM, WN, EK_RESID>(a, ep, s);
     default: return launch_bf16_ek<BM, BN, WM, WN, EK_GENERIC>(a, ep, s);
+  }
+}
+
+// persistent kernel: register epilogues only, K >= 128, and 32-bit buffer offsets for C / aux
+bool ps_ok(const EchoGemmArgs* a, int ek) {
+  if (ek != EK_STORE && ek != EK_SWIGLU && ek != EK_RESID) return false;
+  if (a->K < 128 || a->N % 256) return false;
+  const int64_t lim = (int64_t)1 << 30;  // elements: 32-bit byte offsets (rows up to M + 255)
+  if ((int64_t)(a->M + 255) * a->ldc >= lim || (int64_t)a->M * a->lda >= lim || (int64_t)a->N * a->ldw >= lim)
+    return false;
+  if (ek == EK_RESID && (int64_t)(a->M + 255) * a->ld_aux >= lim) return false;
+  return true;
+}
+
+template <int CP = 0>
+int launch_ps(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
+  switch (ek_of(a)) {
+    case EK_STORE: return launch_ps_ek<EK_STORE, CP>(a, ep, s);
+    case EK_SWIGLU: return launch_ps_ek<EK_SWIGLU, CP>(a, ep, s);
+    case EK_RESID: return launch_ps_ek<EK_RESID, CP>(a, ep, s);
+    default: return ECHO_EINVAL;
   }
 }
 
@@ -827,7 +1140,15 @@ int launch_pp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   }
 }
 
+int g_gemm_stagger = 0;  // echo_gemm_set_diag key 1
+
 }  // namespace
+
+extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
+  if (key != 1 || value < 0) return ECHO_EINVAL;
+  g_gemm_stagger = value;
+  return 0;
+}
 
 extern "C" int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch) {
   const int t = pick_tile(M, N, K, batch);
@@ -850,9 +1171,13 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   Epi ep{a->bias, a->stride_bias, a->aux, a->ld_aux, a->stride_aux, a->gate, a->stride_gate,
          a->epilogue, a->act, a->out_div,
          a->hn_w, a->hn_w_stride, a->hn_rope, a->hn_heads, a->hn_nblk, a->hn_rope_heads, a->hn_seq_len,
-         a->hn_pos0, a->hn_pos_mult, a->hn_eps};
+         a->hn_pos0, a->hn_pos_mult, a->hn_eps, 0};
+  if (a->tile == 14) ep.stagger = g_gemm_stagger;
+  if (a->tile == 15) ep.epi = 99;  // diagnostic: no epilogue
   int t = a->tile > 0 ? a->tile : pick_tile(a->M, a->N, a->K, a->batch);
-  if (a->tile == 0 && t == 1) t = 13;  // 256x256 tiles run the 2-phase ping-pong (bitwise-identical results)
+  // 256x256 tiles run the persistent 2-phase kernel where its register epilogue applies, else the
+  // 2-phase ping-pong (all bitwise-identical results)
+  if (a->tile == 0 && t == 1) t = (a->dtype == ECHO_BF16 && ps_ok(a, ek_of(a))) ? 16 : 13;
   if (headnorm && (a->dtype != ECHO_BF16 || t != 13 || a->N % 128)) {
     // not fused for this shape / dtype: plain store, then the standalone kernel (same results)
     EchoGemmArgs b = *a;
@@ -874,12 +1199,13 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
   if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C) & 15) return ECHO_EALIGN;
   int tail_cfg = 0;
-  const int M1 = (a->tile == 0 && t == 13 && a->batch == 1 && !headnorm) ? split_rows(a->M, a->N, &tail_cfg) : 0;
+  const int M1 = (a->tile == 0 && (t == 13 || t == 16) && a->batch == 1 && !headnorm)
+                     ? split_rows(a->M, a->N, &tail_cfg) : 0;
   if (M1 > 0) {
     // two launches on the same stream: full rounds of the 256x256 kernel, then the row tail
     EchoGemmArgs h = *a, r = *a;
     h.M = M1;
-    h.tile = 13;
+    h.tile = t;
     r.M = a->M - M1;
     r.tile = tail_cfg;
     r.A = (const bf16_t*)a->A + (int64_t)M1 * a->lda;
@@ -902,7 +1228,9 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
     case 10: return launch_pp<4>(a, ep, s);
     case 11: return launch_pp<8>(a, ep, s);
     case 12: return launch_pp<11>(a, ep, s);
-    case 13: return launch_pp2(a, ep, s);
+    case 13: case 14: case 15: return launch_pp2(a, ep, s);
+    case 16: return ps_ok(a, ek_of(a)) ? launch_ps(a, ep, s) : launch_pp2(a, ep, s);
+    case 17: return ps_ok(a, ek_of(a)) ? launch_ps<2>(a, ep, s) : launch_pp2(a, ep, s);
     default: return ECHO_EINVAL;
   }
 }

@@ -73,6 +73,11 @@ int echo_gemm(const EchoGemmArgs* args, void* stream);
 /* Tile configuration echo_gemm picks for a shape when args->tile == 0 (1..5). */
 int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch);
 
+/* Diagnostic knobs for tools/bench_gemm.py (not used by the product path). key 1: start delay
+ * between the 8 first-round workgroup groups of an XCD for `tile` = 14 (the 256x256 kernel with
+ * staggered tile rounds), in 10 ns ticks. */
+int echo_gemm_set_diag(int32_t key, int32_t value);
+
 /* One key/value segment of the joint attention (model.py:246-253): rows of
  * `len[row]` valid tokens (prefix), head h at element offset h*128. */
 typedef struct {

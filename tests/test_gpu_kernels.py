@@ -126,6 +126,35 @@ def test_gemm_pingpong_bitwise(M, N, K):
     assert torch.equal(ref, ops.gemm(a, w, tile=13))
 
 
+@pytest.mark.parametrize("M,N,K", [(4133, 4096, 192), (300, 512, 128), (1, 256, 2048), (8192, 2304, 640)])
+@pytest.mark.parametrize("epi", [L.EPI_STORE, L.EPI_SWIGLU, L.EPI_RESID])
+def test_gemm_persistent_bitwise(M, N, K, epi):
+    """Persistent kernel (tile 16: one workgroup per CU looping over tiles, register epilogue
+    issued after the next tile's prologue DMA) == the 2-phase kernel, bitwise; more tiles than CUs,
+    ragged M, nk = 2/3, and an output that is a column slice of a wider buffer (padding untouched)."""
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    nout = N // 2 if epi == L.EPI_SWIGLU else N
+    g = torch.tanh(torch.randn(nout, device=DEV)).to(BF)
+    h = torch.randn(M, nout + 256, device=DEV).to(BF)
+    outs = []
+    for tile in (13, 16):
+        buf = h.clone()
+        o = buf[:, :nout]
+        if epi == L.EPI_RESID:
+            ops.gemm(a, w, out=o, epilogue=epi, aux=o, gate=g, tile=tile)
+        else:
+            ops.gemm(a, w, out=o, epilogue=epi, tile=tile)
+        assert torch.equal(buf[:, nout:], h[:, nout:])
+        outs.append(buf)
+    assert torch.equal(outs[0], outs[1])
+    if epi == L.EPI_RESID:  # also without gate
+        b0, b1 = h.clone(), h.clone()
+        ops.gemm(a, w, out=b0[:, :nout], epilogue=epi, aux=b0[:, :nout], tile=13)
+        ops.gemm(a, w, out=b1[:, :nout], epilogue=epi, aux=b1[:, :nout], tile=16)
+        assert torch.equal(b0, b1)
+
+
 @pytest.mark.parametrize("epi", [L.EPI_STORE, L.EPI_RESID, L.EPI_F32OUT])
 def test_gemm_row_split_bitwise(epi):
     """Auto-tiled 10240x2048 launches split rows into whole 256x256 rounds + a smaller-tile tail;

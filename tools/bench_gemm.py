@@ -48,7 +48,10 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--torch", action="store_true", help="also time torch.nn.functional.linear (hipBLASLt)")
     ap.add_argument("--shapes", default=None, help="M,N,K[,epi];... overrides the production list")
+    ap.add_argument("--stagger", type=int, default=0, help="tile 14: first-round group delay (10 ns ticks)")
     args = ap.parse_args()
+    if args.stagger:
+        assert L.load().echo_gemm_set_diag(1, args.stagger) == 0
     shapes = SHAPES
     if args.shapes:
         shapes = []
