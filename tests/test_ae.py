@@ -1,0 +1,66 @@
+"""Fish-S1-DAC output path: oracle pinned to the reference's goldens
+(tests/golden/make_golden_ae.py), weight-norm folding, flattening-point crop; GPU parity of the
+HIP decoder (echo_tts_amd.codec) against the goldens and the oracle."""
+import json
+import os
+import sys
+
+import pytest
+import torch
+
+from conftest import GOLDEN, load_golden, load_meta, rel_l2
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import echo_tts_amd  # noqa: E402,F401
+from echo_tts_amd import codec_weights as CW  # noqa: E402
+from oracle import ae_oracle as AO  # noqa: E402
+
+
+_W = {}
+
+
+def weights(dtype):
+    if dtype not in _W:
+        state = CW.synthetic_decode_state()
+        _W[dtype] = CW.decode_weights(state, dtype)
+    return _W[dtype]
+
+
+def cis_table():
+    return CW.reference_buffers()["quantizer.post_module.freqs_cis"]
+
+
+@pytest.mark.parametrize("name,dtype,tol", [("ae_fp32", torch.float32, 1e-6), ("ae_bf16", torch.bfloat16, 1e-6)])
+def test_oracle_matches_reference_decode(name, dtype, tol):
+    """Staged oracle decode vs the reference DAC (same synthetic weights): identical on this CPU
+    (same torch ops in the same order), tolerance only for BLAS-threading reduction order."""
+    g = load_golden(name)
+    comps, mean, scale = CW.synthetic_pca_state()
+    stages = {}
+    audio = AO.ae_decode(g["latents"], weights(dtype), cis_table(), comps, mean, scale, dtype, stages=stages)
+    assert audio.shape == g["audio"].shape
+    for k in ("z_q", "post_module", "upsample_0", "upsample_1", "decoder_0", "decoder_1", "decoder_2"):
+        assert rel_l2(stages[k].float(), g[k]) < tol, (k, rel_l2(stages[k].float(), g[k]))
+    assert rel_l2(audio, g["audio"]) < tol
+
+
+def test_flattening_point_matches_reference():
+    with open(os.path.join(GOLDEN, "flatten.json")) as f:
+        fx = json.load(f)
+    for c in fx["cases"]:
+        d = torch.tensor(c["data"], dtype=torch.float32)
+        assert AO.find_flattening_point(d) == c["point"], c["name"]
+
+
+def test_decode_state_layout():
+    shapes = CW.decode_state_shapes()
+    assert len(shapes) == 214
+    n = sum(int(torch.tensor(s).prod()) for s in shapes.values())
+    assert n == 184196194
+    st = CW.synthetic_decode_state()
+    assert list(CW.iter_missing(st)) == []
+    W = CW.decode_weights(st)
+    w = W["decoder.model.1.block.1.weight"]  # ConvTranspose1d [C_in, C_out, k], norm over dims 1,2
+    assert w.shape == (1536, 768, 16)
+    g = st["decoder.model.1.block.1.conv.parametrizations.weight.original0"]
+    assert torch.allclose(w.reshape(1536, -1).norm(dim=1), g.reshape(-1), rtol=1e-5)
