@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(PKG, "libecho_hip.so")
 
 ECHO_BF16, ECHO_F32 = 0, 1
 EPI_STORE, EPI_SWIGLU, EPI_RESID, EPI_F32OUT, EPI_HEADNORM = 0, 1, 2, 3, 4
-ACT_NONE, ACT_SILU = 0, 1
+ACT_NONE, ACT_SILU, ACT_GELU, ACT_SNAKE = 0, 1, 2, 3
 ERRORS = {-1: "ECHO_EINVAL", -2: "ECHO_EDTYPE", -3: "ECHO_ESHAPE", -4: "ECHO_EALIGN"}
 
 vp, i32, i64, f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
@@ -30,7 +30,8 @@ class GemmArgs(C.Structure):
                 ("epilogue", i32), ("act", i32), ("out_div", f32), ("tile", i32),
                 ("hn_w", vp), ("hn_w_stride", i64), ("hn_rope", vp),
                 ("hn_heads", i32), ("hn_nblk", i32), ("hn_rope_heads", i32), ("hn_seq_len", i32),
-                ("hn_pos0", i32), ("hn_pos_mult", i32), ("hn_eps", f32)]
+                ("hn_pos0", i32), ("hn_pos_mult", i32), ("hn_eps", f32),
+                ("act_alpha", vp), ("conv_c", i32), ("conv_taps", i32), ("conv_dil", i32)]
 
 
 class KVSegment(C.Structure):
@@ -70,6 +71,14 @@ SIGNATURES = {
     "echo_embed": (i32, [i32, vp, vp, vp, i32, i32, vp]),
     "echo_scale_rows": (i32, [i32, vp, i64, i32, i32, f32, vp]),
     "echo_cast_from_f32": (i32, [i32, vp, vp, i64, vp]),
+    "echo_pca_inverse": (i32, [i32, vp, vp, vp, f32, vp, i32, i32, i32, vp]),
+    "echo_snake": (i32, [i32, vp, i64, i64, vp, i64, i64, vp, i32, i32, i32, vp]),
+    "echo_dwconv_layernorm": (i32, [i32, vp, i64, i64, vp, i64, i64, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
+    "echo_ae_rmsnorm": (i32, [i32, vp, i64, vp, vp, i64, i32, i32, f32, vp]),
+    "echo_rope_pairs": (i32, [i32, vp, i64, i32, i32, i32, vp, i32, vp]),
+    "echo_window_attention": (i32, [i32, vp, i64, vp, i64, i32, i32, i32, i32, i32, vp]),
+    "echo_conv_out_tanh": (i32, [i32, vp, i64, i64, vp, vp, vp, i64, i32, i32, i32, vp]),
+    "echo_flattening_point": (i32, [vp, i32, i32, i32, f32, f32, vp, vp]),
     "echo_version": (C.c_char_p, []),
 }
 

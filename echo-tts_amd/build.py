@@ -18,7 +18,7 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(PKG, "libecho_hip.so")
 OBJ = os.path.join(PKG, "build")
-SOURCES = ["gemm.hip", "attention.hip", "elementwise.hip"]
+SOURCES = ["gemm.hip", "attention.hip", "elementwise.hip", "codec.hip"]
 HEADERS = [os.path.join(CSRC, "common.h"), os.path.join(REPO, "include", "echo_hip.h")]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
          "-Wno-unused-result"]

@@ -33,11 +33,37 @@ struct Epi {
   const void* hn_w; int64_t hn_w_stride; const float* hn_rope;
   int hn_heads, hn_nblk, hn_rope_heads, hn_seq_len, hn_pos0, hn_pos_mult; float hn_eps;
   int stagger;  // diagnostic (tile 14): first-round start delay per CU group, 10 ns ticks
+  const void* act_alpha;        // ECHO_ACT_SNAKE
+  int conv_c, conv_taps, conv_dil;  // causal-conv A addressing (echo_hip.h)
 };
 
-__device__ __forceinline__ float epi_pointwise(float v, const Epi& ep) {
+// Element offset added to A for the K-slice starting at k0 in conv mode (0 otherwise): tap
+// t = k0 / conv_c reads rows shifted back by (taps-1-t)*dil, at column k0 - t*conv_c.
+__device__ __forceinline__ int64_t tap_delta(const Epi& ep, int k0, int64_t lda) {
+  if (ep.conv_taps == 0) return 0;
+  const int tap = k0 / ep.conv_c;
+  return -((int64_t)tap * ep.conv_c + (int64_t)(ep.conv_taps - 1 - tap) * ep.conv_dil * lda);
+}
+
+// GELU (exact erf form, nn.GELU default) and Snake (autoencoder.py:97-102) for the epilogues.
+__device__ __forceinline__ float gelu_erf(float x) { return x * 0.5f * (1.0f + erff(x * 0.70710678118654752f)); }
+// bf16 Snake with the reference's rounding after each tensor op:
+// x + round(round(1/round(a + 1e-9)) * round(round(sin(round(a*x)))^2))
+__device__ __forceinline__ float snake_bf16(float x, float a) {
+  const float s = rbf(sinf(rbf(a * x)));
+  const float r = rbf(1.0f / rbf(a + 1e-9f));
+  return rbf(x + rbf(r * rbf(s * s)));
+}
+__device__ __forceinline__ float snake_f32(float x, float a) {
+  const float s = sinf(a * x);
+  return x + (1.0f / (a + 1e-9f)) * (s * s);
+}
+
+__device__ __forceinline__ float epi_pointwise(float v, const Epi& ep, int n) {
   v = rbf(v);
   if (ep.act == ECHO_ACT_SILU) v = rbf(silu_f(v));
+  else if (ep.act == ECHO_ACT_GELU) v = rbf(gelu_erf(v));
+  else if (ep.act == ECHO_ACT_SNAKE) v = snake_bf16(v, bf2f(((const bf16_t*)ep.act_alpha)[n]));
   if (ep.out_div != 0.0f) v = rbf(v / ep.out_div);
   return v;
 }
@@ -91,8 +117,9 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
         for (int r = 0; r < 4; ++r) {
           float x = acc[i][j][r];
           if (EK == EK_GENERIC) {
-            if (biasp) x += bf2f(biasp[min(n0 + wn * TN + nl + r, N - 1)]);
-            x = epi_pointwise(x, ep);
+            const int nc = min(n0 + wn * TN + nl + r, N - 1);
+            if (biasp) x += bf2f(biasp[nc]);
+            x = epi_pointwise(x, ep, nc);
           }
           v[r] = x;  // pack2bf rounds (RNE) exactly once
         }
@@ -291,7 +318,7 @@ gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
       const int row = rb + (lane >> 3);
       const int gc = (lane & 7) ^ ((row >> 1) & 7);
       const int grow = min(m0 + row, M - 1);
-      const bf16_t* src = A + (int64_t)grow * lda + k0 + gc * 8;
+      const bf16_t* src = A + (int64_t)grow * lda + k0 + gc * 8 + tap_delta(ep, k0, lda);
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(As + rb * BK), 16, 0, 0);
     }
@@ -425,10 +452,11 @@ gemm_bf16_pp_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
     }
   // chunk c of K-tile kt into buffer kt&1 (two 1 KiB wave-instructions)
   auto dma = [&](int c, int kt) {
+    const int64_t td = (c == 0 || c == 3) ? tap_delta(ep, kt * BK, lda) : 0;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(dsrc[c][h] + kt * BK),
+          (const __attribute__((address_space(1))) void*)(dsrc[c][h] + kt * BK + td),
           (__attribute__((address_space(3))) void*)(lds + (kt & 1) * STAGE + ddst[c][h]), 16, 0, 0);
   };
 
@@ -568,10 +596,11 @@ gemm_bf16_pp2_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
       ddst[c][h] = (isA ? 0 : BM * BK) + rb * BK;
     }
   auto dma = [&](int c, int kt) {
+    const int64_t td = (c == 0 || c == 3) ? tap_delta(ep, kt * BK, lda) : 0;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(dsrc[c][h] + kt * BK),
+          (const __attribute__((address_space(1))) void*)(dsrc[c][h] + kt * BK + td),
           (__attribute__((address_space(3))) void*)(lds + (kt & 1) * STAGE + ddst[c][h]), 16, 0, 0);
   };
 
@@ -725,7 +754,7 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   };
   const uint32_t lds0 = lds_addr_of(lds);
   auto dma = [&](int c, int kt) __attribute__((always_inline)) {
-    const bf16_t* base = ((c == 0 || c == 3) ? A : W) + kt * BK;
+    const bf16_t* base = ((c == 0 || c == 3) ? A + tap_delta(ep, kt * BK, lda) : W) + kt * BK;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int rb = chunk_row(c, 2 * wid + h);
@@ -928,7 +957,7 @@ gemm_f32_kernel(const float* __restrict__ A, int64_t lda, int64_t sA,
   for (int k0 = 0; k0 < K; k0 += FK) {
     for (int e = threadIdx.x; e < FT * FK; e += 256) {
       const int r = e / FK, kk = e % FK;
-      As[kk][r] = A[(int64_t)min(m0 + r, M - 1) * lda + k0 + kk];
+      As[kk][r] = A[(int64_t)min(m0 + r, M - 1) * lda + k0 + kk + tap_delta(ep, k0, lda)];
       Ws[kk][r] = W[(int64_t)min(n0 + r, N - 1) * ldw + k0 + kk];
     }
     __syncthreads();
@@ -953,6 +982,8 @@ gemm_f32_kernel(const float* __restrict__ A, int64_t lda, int64_t sA,
       const int n = n0 + tx + 16 * j;
       if (bias && ep.epi != ECHO_EPI_SWIGLU) v += bias[min(n, N - 1)];
       if (ep.act == ECHO_ACT_SILU) v = silu_f(v);
+      else if (ep.act == ECHO_ACT_GELU) v = gelu_erf(v);
+      else if (ep.act == ECHO_ACT_SNAKE) v = snake_f32(v, ((const float*)ep.act_alpha)[min(n, N - 1)]);
       if (ep.out_div != 0.0f) v = v / ep.out_div;
       Ct[ty + 16 * i][tx + 16 * j] = v;
     }
@@ -1162,6 +1193,11 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   if (a->epilogue == ECHO_EPI_RESID && !a->aux) return ECHO_EINVAL;
   if (a->epilogue == ECHO_EPI_SWIGLU && (a->N % 32 || a->bias)) return ECHO_EINVAL;
   if (a->epilogue < 0 || a->epilogue > 4) return ECHO_EINVAL;
+  if (a->act < 0 || a->act > ECHO_ACT_SNAKE || (a->act == ECHO_ACT_SNAKE && !a->act_alpha)) return ECHO_EINVAL;
+  if (a->conv_taps < 0 || (a->conv_taps > 0 && (a->conv_c <= 0 || a->conv_dil <= 0 ||
+                                                 (int64_t)a->conv_taps * a->conv_c != a->K ||
+                                                 a->conv_c % (a->dtype == ECHO_BF16 ? 64 : 16))))
+    return ECHO_EINVAL;
   const bool headnorm = a->epilogue == ECHO_EPI_HEADNORM;
   if (headnorm && (a->batch != 1 || !a->hn_w || a->hn_heads <= 0 || a->hn_nblk < 0 || a->hn_seq_len <= 0 ||
                    (int64_t)a->hn_nblk * a->hn_heads * 128 > a->N || (a->hn_rope_heads > 0 && !a->hn_rope) ||
@@ -1171,7 +1207,7 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   Epi ep{a->bias, a->stride_bias, a->aux, a->ld_aux, a->stride_aux, a->gate, a->stride_gate,
          a->epilogue, a->act, a->out_div,
          a->hn_w, a->hn_w_stride, a->hn_rope, a->hn_heads, a->hn_nblk, a->hn_rope_heads, a->hn_seq_len,
-         a->hn_pos0, a->hn_pos_mult, a->hn_eps, 0};
+         a->hn_pos0, a->hn_pos_mult, a->hn_eps, 0, a->act_alpha, a->conv_c, a->conv_taps, a->conv_dil};
   if (a->tile == 14) ep.stagger = g_gemm_stagger;
   if (a->tile == 15) ep.epi = 99;  // diagnostic: no epilogue
   int t = a->tile > 0 ? a->tile : pick_tile(a->M, a->N, a->K, a->batch);

@@ -8,7 +8,7 @@ import ctypes as C
 import os
 import sys
 from dataclasses import dataclass
-from typing import Optional, Sequence
+from typing import Optional, Sequence, Tuple
 
 import torch
 
@@ -79,9 +79,13 @@ class HeadNorm:
 def gemm(a: Tensor, w: Tensor, out: Optional[Tensor] = None, *, bias: Optional[Tensor] = None,
          epilogue: int = L.EPI_STORE, aux: Optional[Tensor] = None, gate: Optional[Tensor] = None,
          act: int = L.ACT_NONE, out_div: float = 0.0, tile: int = 0,
-         head_norm: Optional[HeadNorm] = None) -> Tensor:
+         head_norm: Optional[HeadNorm] = None, act_alpha: Optional[Tensor] = None,
+         conv: Optional[Tuple[int, int]] = None) -> Tensor:
     """out = epilogue(a @ w^T). a [(B,)M,K], w [(B,)N,K]; see include/echo_hip.h for epilogues.
-    head_norm selects ECHO_EPI_HEADNORM (fused q/k norm + RoPE after the store rounding)."""
+    head_norm selects ECHO_EPI_HEADNORM (fused q/k norm + RoPE after the store rounding).
+    conv = (taps, dilation): causal conv as a GEMM — a is the channels-last activation
+    [(B,)L,C] (a view that keeps >= (taps-1)*dilation zero rows of its buffer before row 0),
+    w [N, taps*C] with w[co][tap*C + ci] = weight[co][ci][tap]; act_alpha: Snake alpha [N]."""
     _check_dev(a, w, out, bias, aux, gate, None if head_norm is None else head_norm.w,
                None if head_norm is None else head_norm.rope)
     if head_norm is not None:
@@ -90,6 +94,11 @@ def gemm(a: Tensor, w: Tensor, out: Optional[Tensor] = None, *, bias: Optional[T
         epilogue = L.EPI_HEADNORM
     ba, M, K, lda, sa = _mat(a, "a")
     bw, N, Kw, ldw, sw = _mat(w, "w")
+    conv_c = 0
+    if conv is not None:
+        conv_c, K = K, K * conv[0]
+        if a.storage_offset() < (conv[0] - 1) * conv[1] * lda:
+            raise ValueError("conv input needs (taps-1)*dilation rows of its buffer before row 0")
     if Kw != K:
         raise ValueError(f"K mismatch {K} vs {Kw}")
     if a.dtype != w.dtype:
@@ -130,6 +139,12 @@ def gemm(a: Tensor, w: Tensor, out: Optional[Tensor] = None, *, bias: Optional[T
                 raise ValueError("gate must be [(B,)N]")
             args.gate, args.stride_gate = gate.data_ptr(), (gate.stride(0) if gate.dim() == 2 else 0)
     args.epilogue, args.act, args.out_div, args.tile = epilogue, act, out_div, tile
+    if act == L.ACT_SNAKE:
+        if act_alpha is None or act_alpha.dtype != a.dtype or act_alpha.numel() != N or not act_alpha.is_contiguous():
+            raise ValueError("ACT_SNAKE needs a contiguous alpha [N] of the model dtype")
+        args.act_alpha = act_alpha.data_ptr()
+    if conv is not None:
+        args.conv_c, args.conv_taps, args.conv_dil = conv_c, conv[0], conv[1]
     if head_norm is not None:
         hn = head_norm
         if hn.w.dtype != a.dtype or (hn.rope is not None and hn.rope.dtype != torch.float32):

@@ -33,6 +33,9 @@ enum { ECHO_OK = 0, ECHO_EINVAL = -1, ECHO_EDTYPE = -2, ECHO_ESHAPE = -3, ECHO_E
 /* GEMM epilogues (applied in this order; see echo-tts_amd/csrc/gemm.hip):
  *   v = acc (+ bias[n]);  v = round(v)                       F.linear (model.py:56-62,303-305,...)
  *   act == ECHO_ACT_SILU: v = round(silu(v))                 nn.SiLU in cond_module (model.py:532-538)
+ *   act == ECHO_ACT_GELU: v = round(gelu_erf(v))             ConvNeXt pwconv1 + nn.GELU (autoencoder.py:366-367)
+ *   act == ECHO_ACT_SNAKE: v = snake(v, act_alpha[n]) with the reference's bf16 rounding after
+ *                    every op (fp32: none)                   Snake1d after a conv (autoencoder.py:97-102,886)
  *   out_div != 0:         v = round(v / out_div)             SpeakerEncoder `x / 6.` (model.py:462)
  *   ECHO_EPI_SWIGLU: W rows interleaved in blocks of 16 (w1,w3,w1,w3,...);
  *                    out[m][n] = round(round(silu(a)) * b)   MLP.forward (model.py:307-308)
@@ -45,7 +48,7 @@ enum { ECHO_OK = 0, ECHO_EINVAL = -1, ECHO_EDTYPE = -2, ECHO_ESHAPE = -3, ECHO_E
  *                    the fused QKV(G) projection (model.py:138-142,199-202,221-232); batch == 1
  */
 enum { ECHO_EPI_STORE = 0, ECHO_EPI_SWIGLU = 1, ECHO_EPI_RESID = 2, ECHO_EPI_F32OUT = 3, ECHO_EPI_HEADNORM = 4 };
-enum { ECHO_ACT_NONE = 0, ECHO_ACT_SILU = 1 };
+enum { ECHO_ACT_NONE = 0, ECHO_ACT_SILU = 1, ECHO_ACT_GELU = 2, ECHO_ACT_SNAKE = 3 };
 
 typedef struct {
   int32_t dtype;
@@ -64,6 +67,15 @@ typedef struct {
   const void* hn_w; int64_t hn_w_stride; const float* hn_rope;
   int32_t hn_heads, hn_nblk, hn_rope_heads, hn_seq_len, hn_pos0, hn_pos_mult;
   float hn_eps;
+  /* ECHO_ACT_SNAKE per-column alpha [N] (output dtype) */
+  const void* act_alpha;
+  /* Causal 1-D convolution as a GEMM (conv_taps > 0): K = conv_taps * conv_c and A is the
+   * channels-last activation x (row stride lda) read as the virtual matrix
+   *   A'[t][tap*conv_c + c] = x[t - (conv_taps-1-tap)*conv_dil][c]
+   * i.e. CausalConvNet (autoencoder.py:264-289) with W[co][tap*conv_c + ci] = w[co][ci][tap].
+   * Rows before t = 0 are read from memory: the caller keeps >= (conv_taps-1)*conv_dil zero rows
+   * ahead of A. conv_c % 64 == 0 (bf16) / % 16 == 0 (fp32). */
+  int32_t conv_c, conv_taps, conv_dil;
 } EchoGemmArgs;
 
 /* Replaces every nn.Linear of the DiT and its encoders (F.linear, model.py:56-62,
@@ -178,6 +190,41 @@ int echo_scale_rows(int32_t dtype, void* x, int64_t ldx, int32_t rows, int32_t c
 
 /* fp32 -> dtype cast of n elements (speaker_latent.to(dtype), inference.py:483). */
 int echo_cast_from_f32(int32_t dtype, const float* x, void* y, int64_t n, void* stream);
+
+/* ---- Fish-S1-DAC output path (csrc/codec.hip). Activations are
+ * channels-last [batch][rows][C]; s* arguments are per-item strides in elements. */
+
+/* ae_decode's PCA inverse (inference.py:233): out[r][d] = (lat[r]/scale) . comps[:, d] + mean[d],
+ * fp32 math, stored in dtype. lat [rows, K] fp32, comps [K, D] fp32, mean [D] fp32. */
+int echo_pca_inverse(int32_t dtype, const float* lat, const float* comps, const float* mean, float scale,
+                     void* out, int32_t rows, int32_t K, int32_t D, void* stream);
+/* Snake1d (autoencoder.py:97-108): y = x + (alpha+1e-9)^-1 sin(alpha x)^2 per channel; C % 8 == 0. */
+int echo_snake(int32_t dtype, const void* x, int64_t ldx, int64_t sx, void* y, int64_t ldy, int64_t sy,
+               const void* alpha, int32_t rows, int32_t C, int32_t batch, void* stream);
+/* ConvNeXtBlock head (autoencoder.py:360-364): causal depthwise conv k7 + bias (w_dw [C][7]), then
+ * LayerNorm over C (eps) with ln_w / ln_b. Rows t < 0 of the conv read as zero. C <= 2048. */
+int echo_dwconv_layernorm(int32_t dtype, const void* x, int64_t ldx, int64_t sx, void* y, int64_t ldy, int64_t sy,
+                          const void* w_dw, const void* b_dw, const void* ln_w, const void* ln_b, int32_t rows,
+                          int32_t C, int32_t batch, float eps, void* stream);
+/* RMSNorm of the AE transformer (autoencoder.py:720-731): cast(x * rsqrt(mean(x^2)+eps)) * w. */
+int echo_ae_rmsnorm(int32_t dtype, const void* x, int64_t ldx, const void* w, void* y, int64_t ldy, int32_t rows,
+                    int32_t dim, float eps, void* stream);
+/* apply_rotary_emb (autoencoder.py:815-826) in place on interleaved pairs of [rows][heads*hd];
+ * table bf16 [npos][hd/2][2] (cos, sin), position = row % seq_len. */
+int echo_rope_pairs(int32_t dtype, void* x, int64_t ld, int32_t rows, int32_t heads, int32_t hd,
+                    const void* table_bf16, int32_t seq_len, void* stream);
+/* Window-limited causal attention (autoencoder.py:663-706,762-773): qkv [batch*T][3*heads*64]
+ * (q | k | v, row stride ld), out [batch*T][heads*64]; query t sees keys max(0,t-window+1)..t.
+ * head_dim == 64, window <= 128. */
+int echo_window_attention(int32_t dtype, const void* qkv, int64_t ld, void* out, int64_t ldo, int32_t batch,
+                          int32_t T, int32_t heads, int32_t head_dim, int32_t window, void* stream);
+/* Decoder tail (autoencoder.py:995-996 + .float()): y[t] = tanh(conv_k7(s)[t] + bias) on the
+ * Snake'd input s (>= 6 zero rows before t = 0 in its buffer); w [7][C] tap-major; y fp32. */
+int echo_conv_out_tanh(int32_t dtype, const void* s, int64_t lds, int64_t ss, const void* w, const void* bias,
+                       float* y, int64_t sy, int32_t rows, int32_t C, int32_t batch, void* stream);
+/* find_flattening_point (inference.py:315-330) of x [L][D] fp32 -> *out (device int32). */
+int echo_flattening_point(const float* x, int32_t L, int32_t D, int32_t window, float std_threshold, float target,
+                          int32_t* out, void* stream);
 
 /* Library identification (build stamp) — for load checks. */
 const char* echo_version(void);
