@@ -52,6 +52,11 @@ class StepArgs(C.Structure):
                 ("omt", f32), ("ratio", f32), ("inv_omt", f32), ("dt", f32)]
 
 
+class RvqWeights(C.Structure):
+    _fields_ = [("w_in", vp), ("b_in", vp), ("cbn", vp), ("csq", vp), ("cb", vp), ("w_out", vp), ("b_out", vp),
+                ("codebook_sizes", i32 * 16), ("nq", i32), ("codebook_dim", i32)]
+
+
 # name -> (restype, argtypes); must match include/echo_hip.h exactly
 SIGNATURES = {
     "echo_gemm": (i32, [C.POINTER(GemmArgs), vp]),
@@ -79,6 +84,9 @@ SIGNATURES = {
     "echo_window_attention": (i32, [i32, vp, i64, vp, i64, i32, i32, i32, i32, i32, vp]),
     "echo_conv_out_tanh": (i32, [i32, vp, i64, i64, vp, vp, vp, i64, i32, i32, i32, vp]),
     "echo_flattening_point": (i32, [vp, i32, i32, i32, f32, f32, vp, vp]),
+    "echo_conv_in": (i32, [i32, vp, i64, vp, vp, vp, i64, i64, i32, i32, i32, vp]),
+    "echo_rvq_encode": (i32, [i32, vp, i64, i32, i32, i32, C.POINTER(RvqWeights), vp, vp, i64, vp, vp, f32, vp,
+                              i32, vp]),
     "echo_version": (C.c_char_p, []),
 }
 

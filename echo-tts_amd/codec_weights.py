@@ -46,6 +46,24 @@ class FishAEConfig:
     t_norm_eps: float = 1e-5
     pca_dim: int = 80               # echo latent size (PCA components)
     hop: int = 2048                 # audio samples per latent (AE_DOWNSAMPLE_FACTOR)
+    # encode path (Encoder + quantizer downsample / pre_module / RVQ, autoencoder.py:903-929,376-484)
+    encoder_dim: int = 64
+    encoder_rates: Tuple[int, ...] = (2, 4, 8, 8)
+    enc_t_layers: int = 4           # transformer of the last EncoderBlock (encoder_transformer_layers)
+    enc_window: int = 512
+    enc_block_size: int = 16384
+    n_codebooks: int = 9            # residual quantizer
+    codebook_size: int = 1024
+    semantic_codebook_size: int = 4096
+    codebook_dim: int = 8
+
+    def encoder_stage_dims(self) -> List[Tuple[int, int, int]]:
+        """(residual-unit dim, output dim, stride) of each EncoderBlock (autoencoder.py:914-922)."""
+        out, d = [], self.encoder_dim
+        for s in self.encoder_rates:
+            d *= 2
+            out.append((d // 2, d, s))
+        return out
 
     def stage_dims(self) -> List[Tuple[int, int, int]]:
         """(input_dim, output_dim, stride) of each DecoderBlock (autoencoder.py:986-994)."""
@@ -53,15 +71,12 @@ class FishAEConfig:
                 for i, s in enumerate(self.decoder_rates)]
 
 
-def decode_state_shapes(cfg: FishAEConfig = FishAEConfig()) -> Dict[str, Shape]:
-    """Every decode-path parameter of the reference DAC with its shape (buffers excluded)."""
-    out: Dict[str, Shape] = {}
-    D, F = cfg.latent_dim, cfg.t_ffn
-    pm = "quantizer.post_module"
-    for i in range(cfg.t_layers):
-        b = f"{pm}.layers.{i}"
-        out[f"{b}.attention.wqkv.weight"] = (3 * cfg.t_heads * cfg.t_head_dim, D)
-        out[f"{b}.attention.wo.weight"] = (D, cfg.t_heads * cfg.t_head_dim)
+def _transformer_shapes(out: Dict[str, Shape], p: str, n_layers: int, D: int, heads: int, hd: int, F: int):
+    """WindowLimitedTransformer parameters (autoencoder.py:554-802), buffers excluded."""
+    for i in range(n_layers):
+        b = f"{p}.layers.{i}"
+        out[f"{b}.attention.wqkv.weight"] = (3 * heads * hd, D)
+        out[f"{b}.attention.wo.weight"] = (D, heads * hd)
         out[f"{b}.feed_forward.w1.weight"] = (F, D)
         out[f"{b}.feed_forward.w3.weight"] = (F, D)
         out[f"{b}.feed_forward.w2.weight"] = (D, F)
@@ -69,24 +84,92 @@ def decode_state_shapes(cfg: FishAEConfig = FishAEConfig()) -> Dict[str, Shape]:
         out[f"{b}.attention_norm.weight"] = (D,)
         out[f"{b}.attention_layer_scale.gamma"] = (D,)
         out[f"{b}.ffn_layer_scale.gamma"] = (D,)
-    out[f"{pm}.norm.weight"] = (D,)
+    out[f"{p}.norm.weight"] = (D,)
+
+
+def _convnext_shapes(out: Dict[str, Shape], p: str, D: int):
+    """ConvNeXtBlock parameters (autoencoder.py:333-358)."""
+    out[f"{p}.gamma"] = (D,)
+    out[f"{p}.dwconv.conv.weight"] = (D, 1, 7)
+    out[f"{p}.dwconv.conv.bias"] = (D,)
+    out[f"{p}.norm.weight"] = (D,)
+    out[f"{p}.norm.bias"] = (D,)
+    out[f"{p}.pwconv1.weight"] = (4 * D, D)
+    out[f"{p}.pwconv1.bias"] = (4 * D,)
+    out[f"{p}.pwconv2.weight"] = (D, 4 * D)
+    out[f"{p}.pwconv2.bias"] = (D,)
+
+
+def _wn_shapes(out: Dict[str, Shape], conv: str, shape: Shape):
+    """torch weight_norm(dim=0) parametrization of a conv: gain g [C_out, 1, 1], direction v."""
+    out[f"{conv}.parametrizations.weight.original0"] = (shape[0], 1, 1)
+    out[f"{conv}.parametrizations.weight.original1"] = shape
+
+
+def _residual_unit_shapes(out: Dict[str, Shape], ru: str, dim: int):
+    """ResidualUnit (autoencoder.py:879-890): Snake, WN conv k7, Snake, WN conv k1."""
+    out[f"{ru}.0.alpha"] = (1, dim, 1)
+    _wn_shapes(out, f"{ru}.1.conv", (dim, dim, 7))
+    out[f"{ru}.1.conv.bias"] = (dim,)
+    out[f"{ru}.2.alpha"] = (1, dim, 1)
+    _wn_shapes(out, f"{ru}.3.conv", (dim, dim, 1))
+    out[f"{ru}.3.conv.bias"] = (dim,)
+
+
+def encode_state_shapes(cfg: "FishAEConfig" = None) -> Dict[str, Shape]:
+    """Every encode-path parameter of the reference DAC (`DAC.encode_zq`, autoencoder.py:1117-1126):
+    encoder (:903-929, EncoderBlock :839-877), quantizer.downsample (:391-397), pre_module and the
+    semantic + residual VQ stacks (:117-158,160-232). Buffers excluded."""
+    cfg = cfg or FishAEConfig()
+    out: Dict[str, Shape] = {}
+    _wn_shapes(out, "encoder.block.0.conv", (cfg.encoder_dim, 1, 7))
+    out["encoder.block.0.conv.bias"] = (cfg.encoder_dim,)
+    n = len(cfg.encoder_rates)
+    for i, (half, d, s) in enumerate(cfg.encoder_stage_dims()):
+        b = f"encoder.block.{i + 1}.block"
+        for r in range(3):
+            _residual_unit_shapes(out, f"{b}.{r}.block", half)
+        out[f"{b}.3.alpha"] = (1, half, 1)
+        _wn_shapes(out, f"{b}.4.conv", (d, half, 2 * s))
+        out[f"{b}.4.conv.bias"] = (d,)
+        if i == n - 1 and cfg.enc_t_layers:
+            _transformer_shapes(out, f"{b}.5", cfg.enc_t_layers, d, d // 64, 64, 3 * d)
+    d = cfg.encoder_stage_dims()[-1][1]
+    out[f"encoder.block.{n + 1}.alpha"] = (1, d, 1)
+    _wn_shapes(out, f"encoder.block.{n + 2}.conv", (cfg.latent_dim, d, 3))
+    out[f"encoder.block.{n + 2}.conv.bias"] = (cfg.latent_dim,)
+    D = cfg.latent_dim
+    for j, f in enumerate(cfg.upsample_factors):
+        p = f"quantizer.downsample.{j}"
+        out[f"{p}.0.conv.weight"] = (D, D, f)
+        out[f"{p}.0.conv.bias"] = (D,)
+        _convnext_shapes(out, f"{p}.1", D)
+    _transformer_shapes(out, "quantizer.pre_module", cfg.t_layers, D, cfg.t_heads, cfg.t_head_dim, cfg.t_ffn)
+    for name, nq, size in (("semantic_quantizer", 1, cfg.semantic_codebook_size),
+                           ("quantizer", cfg.n_codebooks, cfg.codebook_size)):
+        for q in range(nq):
+            p = f"quantizer.{name}.quantizers.{q}"
+            _wn_shapes(out, f"{p}.in_proj", (cfg.codebook_dim, D, 1))
+            out[f"{p}.in_proj.bias"] = (cfg.codebook_dim,)
+            _wn_shapes(out, f"{p}.out_proj", (D, cfg.codebook_dim, 1))
+            out[f"{p}.out_proj.bias"] = (D,)
+            out[f"{p}.codebook.weight"] = (size, cfg.codebook_dim)
+    return out
+
+
+def decode_state_shapes(cfg: FishAEConfig = FishAEConfig()) -> Dict[str, Shape]:
+    """Every decode-path parameter of the reference DAC with its shape (buffers excluded)."""
+    out: Dict[str, Shape] = {}
+    D = cfg.latent_dim
+    _transformer_shapes(out, "quantizer.post_module", cfg.t_layers, D, cfg.t_heads, cfg.t_head_dim, cfg.t_ffn)
     for j, f in enumerate(cfg.upsample_factors):
         u = f"quantizer.upsample.{j}"
         out[f"{u}.0.conv.weight"] = (D, D, f)
         out[f"{u}.0.conv.bias"] = (D,)
-        out[f"{u}.1.gamma"] = (D,)
-        out[f"{u}.1.dwconv.conv.weight"] = (D, 1, 7)
-        out[f"{u}.1.dwconv.conv.bias"] = (D,)
-        out[f"{u}.1.norm.weight"] = (D,)
-        out[f"{u}.1.norm.bias"] = (D,)
-        out[f"{u}.1.pwconv1.weight"] = (4 * D, D)
-        out[f"{u}.1.pwconv1.bias"] = (4 * D,)
-        out[f"{u}.1.pwconv2.weight"] = (D, 4 * D)
-        out[f"{u}.1.pwconv2.bias"] = (D,)
+        _convnext_shapes(out, f"{u}.1", D)
 
     def wn(prefix: str, shape: Shape):
-        out[f"{prefix}.conv.parametrizations.weight.original0"] = (shape[0], 1, 1)
-        out[f"{prefix}.conv.parametrizations.weight.original1"] = shape
+        _wn_shapes(out, f"{prefix}.conv", shape)
 
     wn("decoder.model.0", (cfg.decoder_dim, D, 7))
     out["decoder.model.0.conv.bias"] = (cfg.decoder_dim,)
@@ -123,17 +206,24 @@ def synthetic_tensor(key: str, shape: Shape) -> torch.Tensor:
         return 1.0 + 0.1 * x
     if key.endswith("gamma"):
         return 0.1 + 0.01 * x
+    if key.endswith("codebook.weight"):
+        return x
     return x * 0.02
+
+
+def rope_table(block_size: int, head_dim: int = 64, base: float = 10000.0) -> torch.Tensor:
+    """precompute_freqs_cis (autoencoder.py:805-812): [block_size, head_dim/2, 2] in bf16."""
+    n = head_dim
+    freqs = 1.0 / (base ** (torch.arange(0, n, 2)[: n // 2].float() / n))
+    t = torch.arange(block_size)
+    freqs = torch.outer(t, freqs)
+    cis = torch.polar(torch.ones_like(freqs), freqs)
+    return torch.stack([cis.real, cis.imag], dim=-1).to(torch.bfloat16)
 
 
 def reference_buffers(cfg: FishAEConfig = FishAEConfig()) -> Dict[str, torch.Tensor]:
     """post_module buffers exactly as the reference builds them (bf16 rope table, bool mask)."""
-    n = cfg.t_head_dim
-    freqs = 1.0 / (cfg.t_rope_base ** (torch.arange(0, n, 2)[: n // 2].float() / n))
-    t = torch.arange(cfg.t_block_size)
-    freqs = torch.outer(t, freqs)
-    cis = torch.polar(torch.ones_like(freqs), freqs)
-    cache = torch.stack([cis.real, cis.imag], dim=-1).to(torch.bfloat16)
+    cache = rope_table(cfg.t_block_size, cfg.t_head_dim, cfg.t_rope_base)
     mask = torch.tril(torch.ones(cfg.t_block_size, cfg.t_block_size, dtype=torch.bool))
     return {"quantizer.post_module.freqs_cis": cache, "quantizer.post_module.causal_mask": mask}
 
@@ -165,13 +255,21 @@ def fold_weight_norm(g: torch.Tensor, v: torch.Tensor, dtype: torch.dtype) -> to
     return torch._weight_norm(v.to(dtype), g.to(dtype), 0)
 
 
-def decode_weights(state: Dict[str, torch.Tensor], dtype: torch.dtype = torch.float32,
-                   cfg: FishAEConfig = FishAEConfig()) -> Dict[str, torch.Tensor]:
-    """Decode-path tensors in `dtype` with weight norm folded: '<prefix>.weight' per WN conv."""
+def synthetic_encode_state(cfg: FishAEConfig = FishAEConfig(), dtype: torch.dtype = torch.float32) -> Dict[str, torch.Tensor]:
+    """Encode-path parameters under the same per-key recipe (codebooks: plain randn)."""
+    return {k: synthetic_tensor(k, s).to(dtype) for k, s in sorted(encode_state_shapes(cfg).items())}
+
+
+def _fold(state: Dict[str, torch.Tensor], shapes: Dict[str, Shape], dtype: torch.dtype) -> Dict[str, torch.Tensor]:
+    """Tensors of `shapes` in `dtype` with weight norm folded: '<module>.weight' per WN conv
+    ('decoder.model.0.conv.parametrizations.weight.original0' -> 'decoder.model.0.weight',
+    '...in_proj.parametrizations.weight.original0' -> '...in_proj.weight')."""
     out: Dict[str, torch.Tensor] = {}
-    for k in decode_state_shapes(cfg):
+    for k in shapes:
         if k.endswith("original0"):
-            p = k[: -len(".conv.parametrizations.weight.original0")]
+            p = k[: -len(".parametrizations.weight.original0")]
+            if p.endswith(".conv"):
+                p = p[: -len(".conv")]
             out[f"{p}.weight"] = fold_weight_norm(state[k], state[k.replace("original0", "original1")], dtype)
         elif k.endswith("original1"):
             continue
@@ -180,8 +278,21 @@ def decode_weights(state: Dict[str, torch.Tensor], dtype: torch.dtype = torch.fl
     return out
 
 
-def iter_missing(state: Dict[str, torch.Tensor], cfg: FishAEConfig = FishAEConfig()) -> Iterator[str]:
-    for k, s in decode_state_shapes(cfg).items():
+def decode_weights(state: Dict[str, torch.Tensor], dtype: torch.dtype = torch.float32,
+                   cfg: FishAEConfig = FishAEConfig()) -> Dict[str, torch.Tensor]:
+    """Decode-path tensors in `dtype` with weight norm folded: '<prefix>.weight' per WN conv."""
+    return _fold(state, decode_state_shapes(cfg), dtype)
+
+
+def encode_weights(state: Dict[str, torch.Tensor], dtype: torch.dtype = torch.float32,
+                   cfg: FishAEConfig = FishAEConfig()) -> Dict[str, torch.Tensor]:
+    """Encode-path tensors in `dtype` with weight norm folded (same naming as decode_weights)."""
+    return _fold(state, encode_state_shapes(cfg), dtype)
+
+
+def iter_missing(state: Dict[str, torch.Tensor], cfg: FishAEConfig = FishAEConfig(),
+                 shapes: Dict[str, Shape] = None) -> Iterator[str]:
+    for k, s in (shapes if shapes is not None else decode_state_shapes(cfg)).items():
         if k not in state:
             yield k
         elif tuple(state[k].shape) != s:

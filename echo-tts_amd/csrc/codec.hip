@@ -168,28 +168,22 @@ __global__ void __launch_bounds__(256) rope_pairs_kernel(T* __restrict__ x, int6
 // ---- window-limited causal attention, head_dim 64 (Attention.forward with the
 // WindowLimitedTransformer mask, autoencoder.py:663-706,762-773): query t sees keys
 // [max(0, t-window+1), t] of its own item. One block = 64 queries of one (item, head), 4 lanes per
-// query (16 dims each); K/V of the block's key range staged in LDS as fp32; online softmax, fp32.
-constexpr int AQ = 64, AHD = 64, AWMAX = 128;
+// query (16 dims each). The block's key range [q0-window+1, q0+63] is walked in chunks of AKC keys
+// staged in LDS as fp32 (any window: 128 for pre/post_module, 512 for the encoder transformer);
+// every query visits its keys in increasing order with an online fp32 softmax.
+constexpr int AQ = 64, AHD = 64, AKC = 128;
 template <typename T>
 __global__ void __launch_bounds__(256) window_attn_kernel(const T* __restrict__ qkv, int64_t ld, T* __restrict__ out,
                                                           int64_t ldo, int T_, int heads, int window, float scale) {
-  __shared__ float ks[AQ + AWMAX - 1][AHD];
-  __shared__ float vs[AQ + AWMAX - 1][AHD];
+  __shared__ float ks[AKC][AHD];
+  __shared__ float vs[AKC][AHD];
   const int q0 = blockIdx.x * AQ;
   const int h = blockIdx.y;
   const int b = blockIdx.z;
   const int kbeg = max(0, q0 - window + 1);
   const int kend = min(T_ - 1, q0 + AQ - 1);
-  const int nk = kend - kbeg + 1;
   const T* base = qkv + (int64_t)b * T_ * ld;
   const int kc = heads * AHD;
-  for (int e = threadIdx.x; e < nk * AHD; e += 256) {
-    const int j = e / AHD, d = e % AHD;
-    const T* row = base + (int64_t)(kbeg + j) * ld + h * AHD + d;
-    ks[j][d] = ldf<T>(row + kc);
-    vs[j][d] = ldf<T>(row + 2 * kc);
-  }
-  __syncthreads();
   const int ql = threadIdx.x >> 2, part = threadIdx.x & 3;
   const int t = q0 + ql;
   const int tq = min(t, T_ - 1);
@@ -198,27 +192,218 @@ __global__ void __launch_bounds__(256) window_attn_kernel(const T* __restrict__ 
 #pragma unroll
   for (int d = 0; d < 16; ++d) { q[d] = ldf<T>(qp + d); acc[d] = 0.f; }
   float m = -INFINITY, l = 0.f;
-  const int j0 = max(0, tq - window + 1) - kbeg, j1 = tq - kbeg;
-  for (int j = j0; j <= j1; ++j) {
-    float s = 0.f;
+  const int jlo = max(0, tq - window + 1), jhi = tq;
+  for (int c0 = kbeg; c0 <= kend; c0 += AKC) {
+    const int nk = min(AKC, kend - c0 + 1);
+    __syncthreads();
+    for (int e = threadIdx.x; e < nk * AHD; e += 256) {
+      const int j = e / AHD, d = e % AHD;
+      const T* row = base + (int64_t)(c0 + j) * ld + h * AHD + d;
+      ks[j][d] = ldf<T>(row + kc);
+      vs[j][d] = ldf<T>(row + 2 * kc);
+    }
+    __syncthreads();
+    const int j0 = max(jlo, c0) - c0, j1 = min(jhi, c0 + nk - 1) - c0;
+    for (int j = j0; j <= j1; ++j) {
+      float s = 0.f;
 #pragma unroll
-    for (int d = 0; d < 16; ++d) s += q[d] * ks[j][part * 16 + d];
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s *= scale;
-    const float mn = fmaxf(m, s);
-    const float corr = __expf(m - mn);
-    const float p = __expf(s - mn);
-    l = l * corr + p;
+      for (int d = 0; d < 16; ++d) s += q[d] * ks[j][part * 16 + d];
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      s *= scale;
+      const float mn = fmaxf(m, s);
+      const float corr = __expf(m - mn);
+      const float p = __expf(s - mn);
+      l = l * corr + p;
 #pragma unroll
-    for (int d = 0; d < 16; ++d) acc[d] = acc[d] * corr + p * vs[j][part * 16 + d];
-    m = mn;
+      for (int d = 0; d < 16; ++d) acc[d] = acc[d] * corr + p * vs[j][part * 16 + d];
+      m = mn;
+    }
   }
   if (t >= T_) return;
   T* op = out + ((int64_t)b * T_ + t) * ldo + h * AHD + part * 16;
   const float inv = 1.0f / l;
 #pragma unroll
   for (int d = 0; d < 16; ++d) stf<T>(op + d, acc[d] * inv);
+}
+
+// ---- encoder input conv (Encoder.block[0], autoencoder.py:913): causal WN conv k7, 1 -> C
+// channels, on the raw audio [batch][L] (AE dtype): y[t][o] = b[o] + sum_k w[o][k] x[t-6+k]
+// (x[<0] = 0), rounded once; written channels-last into the conv buffer rows.
+template <typename T>
+__global__ void __launch_bounds__(256) conv_in_kernel(const T* __restrict__ x, int64_t sx, const T* __restrict__ w,
+                                                      const T* __restrict__ bias, T* __restrict__ y, int64_t ldy,
+                                                      int64_t sy, int L, int C) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)L * C) return;
+  const int t = (int)(i / C), o = (int)(i % C);
+  const T* xb = x + blockIdx.y * sx;
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const int tt = t - 6 + k;
+    if (tt >= 0) acc += ldf<T>(w + o * 7 + k) * ldf<T>(xb + tt);
+  }
+  stf<T>(y + blockIdx.y * sy + (int64_t)t * ldy + o, acc + ldf<T>(bias + o));
+}
+
+// ---- residual VQ encode + from_codes + PCA projection, one workgroup per latent frame.
+// DownsampleResidualVectorQuantize.forward's code path (autoencoder.py:451-471): the semantic VQ,
+// then the RVQ stages on the running residual; each VectorQuantize.forward (:130-137):
+//   z_e = in_proj(r) (WN conv k1, D -> 8);   e = F.normalize(z_e) (x / max(|x|, 1e-12));
+//   dist_j = |e|^2 - 2 e.c_j + |c_j|^2 over the l2-normalised codebook; code = first argmin;
+//   q = out_proj(z_e + (cb[code] - z_e));   r -= q.
+// Then DAC.encode_zq (:1117-1126): z_q = out_proj(cb[code_0]) + sum_i out_proj(cb[code_i]) and
+// ae_encode's PCA (inference.py:226-228): lat = ((float(z_q) - mean) @ comps^T) * scale.
+// Every value the reference materialises is rounded to T (bf16 mode) where it would be.
+// Thread t owns channels [4t, 4t+4) of D = 1024; reductions: wave shuffles + LDS across 4 waves.
+constexpr int VQ_D = 1024, VQ_CD = 8, VQ_MAXQ = 16, VQ_MAXPCA = 128;
+struct RvqArgs {
+  const void* w_in;    // [nq][8][D]
+  const void* b_in;    // [nq][8]
+  const void* cbn;     // normalised codebooks, concatenated [sum sizes][8]
+  const void* csq;     // |cbn_j|^2 per entry (reference rounding), [sum sizes]
+  const void* cb;      // raw codebooks [sum sizes][8]
+  const void* w_out;   // [nq][D][8]
+  const void* b_out;   // [nq][D]
+  int cb_off[VQ_MAXQ + 1];
+  int nq;
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) rvq_encode_kernel(const T* __restrict__ z, int64_t ldz, RvqArgs a,
+                                                         int32_t* __restrict__ codes, int T_, T* __restrict__ zq_out,
+                                                         int64_t ldq, const float* __restrict__ comps,
+                                                         const float* __restrict__ mean, float scale,
+                                                         float* __restrict__ lat, int npca) {
+  __shared__ float red[4][VQ_MAXPCA];
+  __shared__ float e_s[VQ_CD], st_s[VQ_CD];
+  __shared__ float bd[4];
+  __shared__ int bi[4];
+  const int row = blockIdx.x;  // b * T_ + t
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int c0 = tid * 4;
+  const T* w_in = (const T*)a.w_in;
+  const T* b_in = (const T*)a.b_in;
+  const T* cbn = (const T*)a.cbn;
+  const T* csq = (const T*)a.csq;
+  const T* cb = (const T*)a.cb;
+  const T* w_out = (const T*)a.w_out;
+  const T* b_out = (const T*)a.b_out;
+  float r[4], zs[4], zr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { r[i] = ldf<T>(z + (int64_t)row * ldz + c0 + i); zs[i] = 0.f; zr[i] = 0.f; }
+  for (int q = 0; q < a.nq; ++q) {
+    // z_e = in_proj(r): 8 dot products of length D
+    float p[VQ_CD];
+#pragma unroll
+    for (int o = 0; o < VQ_CD; ++o) {
+      const T* wr = w_in + ((int64_t)q * VQ_CD + o) * VQ_D + c0;
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc += ldf<T>(wr + i) * r[i];
+      p[o] = wave_sum(acc);
+    }
+    if (lane == 0)
+#pragma unroll
+      for (int o = 0; o < VQ_CD; ++o) red[wv][o] = p[o];
+    __syncthreads();
+    if (tid == 0) {
+      float ze[VQ_CD], n2 = 0.f;
+#pragma unroll
+      for (int o = 0; o < VQ_CD; ++o) {
+        ze[o] = rnd<T>(red[0][o] + red[1][o] + red[2][o] + red[3][o] + ldf<T>(b_in + q * VQ_CD + o));
+        n2 += ze[o] * ze[o];
+      }
+      const float n = fmaxf(rnd<T>(sqrtf(n2)), 1e-12f);
+#pragma unroll
+      for (int o = 0; o < VQ_CD; ++o) { e_s[o] = rnd<T>(ze[o] / n); st_s[o] = ze[o]; }
+    }
+    __syncthreads();
+    float e[VQ_CD], esq = 0.f;
+#pragma unroll
+    for (int o = 0; o < VQ_CD; ++o) { e[o] = e_s[o]; esq += e[o] * e[o]; }
+    esq = rnd<T>(esq);
+    // nearest normalised codebook entry: first index of the minimum distance
+    const int off = a.cb_off[q], size = a.cb_off[q + 1] - off;
+    float best = INFINITY;
+    int bidx = 0x7fffffff;
+    for (int j = tid; j < size; j += 256) {
+      const T* cj = cbn + (int64_t)(off + j) * VQ_CD;
+      float dot = 0.f;
+#pragma unroll
+      for (int o = 0; o < VQ_CD; ++o) dot += e[o] * ldf<T>(cj + o);
+      const float d = rnd<T>(rnd<T>(esq - 2.0f * rnd<T>(dot)) + ldf<T>(csq + off + j));
+      if (d < best) { best = d; bidx = j; }  // j increases per thread: keeps the first minimum
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bidx, o, 64);
+      if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+    }
+    if (lane == 0) { bd[wv] = best; bi[wv] = bidx; }
+    __syncthreads();
+    int code = bi[0];
+    float cd = bd[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w)
+      if (bd[w] < cd || (bd[w] == cd && bi[w] < code)) { cd = bd[w]; code = bi[w]; }
+    if (tid == 0) codes[((int64_t)(row / T_) * a.nq + q) * T_ + (row % T_)] = code;
+    // straight-through input and out_proj for the residual; raw code vector for from_codes
+    float stv[VQ_CD], cv[VQ_CD];
+    const T* craw = cb + (int64_t)(off + code) * VQ_CD;
+#pragma unroll
+    for (int o = 0; o < VQ_CD; ++o) {
+      cv[o] = ldf<T>(craw + o);
+      stv[o] = rnd<T>(st_s[o] + rnd<T>(cv[o] - st_s[o]));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const T* wr = w_out + ((int64_t)q * VQ_D + c0 + i) * VQ_CD;
+      const float bo = ldf<T>(b_out + (int64_t)q * VQ_D + c0 + i);
+      float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+      for (int o = 0; o < VQ_CD; ++o) {
+        const float wo = ldf<T>(wr + o);
+        a1 += wo * stv[o];
+        a2 += wo * cv[o];
+      }
+      const float qv = rnd<T>(a1 + bo), qc = rnd<T>(a2 + bo);
+      r[i] = rnd<T>(r[i] - qv);
+      if (q == 0) zs[i] = qc;
+      else zr[i] = (q == 1) ? qc : rnd<T>(zr[i] + qc);
+    }
+    __syncthreads();  // red / e_s / bd reused by the next stage
+  }
+  float zq[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    zq[i] = a.nq > 1 ? rnd<T>(zs[i] + zr[i]) : zs[i];
+    if (zq_out) stf<T>(zq_out + (int64_t)row * ldq + c0 + i, zq[i]);
+  }
+  // PCA projection: npca dot products of length D in fp32
+  for (int j0 = 0; j0 < npca; j0 += VQ_MAXPCA) {
+    const int nj = min(VQ_MAXPCA, npca - j0);
+    for (int j = 0; j < nj; ++j) {
+      const float* cr = comps + (int64_t)(j0 + j) * VQ_D + c0;
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc += (zq[i] - mean[c0 + i]) * cr[i];
+      acc = wave_sum(acc);
+      if (lane == 0) red[wv][j] = acc;
+    }
+    __syncthreads();
+    for (int j = tid; j < nj; j += 256)
+      lat[(int64_t)row * npca + j0 + j] = (red[0][j] + red[1][j] + red[2][j] + red[3][j]) * scale;
+    __syncthreads();
+  }
 }
 
 // ---- output conv + tanh (Decoder tail, autoencoder.py:995-996): y[t] = tanh(b + sum over 7 taps
@@ -361,8 +546,7 @@ extern "C" int echo_rope_pairs(int32_t dtype, void* x, int64_t ld, int32_t rows,
 extern "C" int echo_window_attention(int32_t dtype, const void* qkv, int64_t ld, void* out, int64_t ldo,
                                      int32_t batch, int32_t T, int32_t heads, int32_t head_dim, int32_t window,
                                      void* stream) {
-  if (!qkv || !out || batch <= 0 || T < 0 || heads <= 0 || head_dim != AHD || window <= 0 || window > AWMAX)
-    return ECHO_EINVAL;
+  if (!qkv || !out || batch <= 0 || T < 0 || heads <= 0 || head_dim != AHD || window <= 0) return ECHO_EINVAL;
   if (T == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   dim3 g((T + AQ - 1) / AQ, heads, batch);
@@ -400,6 +584,48 @@ extern "C" int echo_flattening_point(const float* x, int32_t L, int32_t D, int32
   if (L > 0)
     hipLaunchKernelGGL(flatten_kernel, dim3((L + 255) / 256), dim3(256), 0, s, x, L, D, window, std_threshold,
                        target, (int*)out);
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int echo_conv_in(int32_t dtype, const void* x, int64_t sx, const void* w, const void* bias, void* y,
+                            int64_t ldy, int64_t sy, int32_t L, int32_t C, int32_t batch, void* stream) {
+  if (!x || !w || !bias || !y || L < 0 || C <= 0 || batch <= 0 || ldy < C) return ECHO_EINVAL;
+  if (L == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = (int64_t)L * C;
+  dim3 g((unsigned)((n + 255) / 256), batch);
+  ECHO_DISPATCH(dtype,
+      hipLaunchKernelGGL(conv_in_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)x, sx, (const bf16_t*)w,
+                         (const bf16_t*)bias, (bf16_t*)y, ldy, sy, L, C),
+      hipLaunchKernelGGL(conv_in_kernel<float>, g, dim3(256), 0, s, (const float*)x, sx, (const float*)w,
+                         (const float*)bias, (float*)y, ldy, sy, L, C));
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int echo_rvq_encode(int32_t dtype, const void* z, int64_t ldz, int32_t rows, int32_t T, int32_t D,
+                               const EchoRvqWeights* wts, int32_t* codes, void* zq, int64_t ldq, const float* comps,
+                               const float* mean, float scale, float* lat, int32_t npca, void* stream) {
+  if (!z || !wts || !codes || !comps || !mean || !lat || rows < 0 || T <= 0 || rows % T || D != VQ_D ||
+      ldz < D || (zq && ldq < D) || npca <= 0 || wts->nq <= 0 || wts->nq > VQ_MAXQ || wts->codebook_dim != VQ_CD ||
+      !wts->w_in || !wts->b_in || !wts->cbn || !wts->csq || !wts->cb || !wts->w_out || !wts->b_out)
+    return ECHO_EINVAL;
+  if (rows == 0) return 0;
+  RvqArgs a;
+  a.w_in = wts->w_in; a.b_in = wts->b_in; a.cbn = wts->cbn; a.csq = wts->csq; a.cb = wts->cb;
+  a.w_out = wts->w_out; a.b_out = wts->b_out; a.nq = wts->nq;
+  a.cb_off[0] = 0;
+  for (int q = 0; q < wts->nq; ++q) {
+    if (wts->codebook_sizes[q] <= 0) return ECHO_EINVAL;
+    a.cb_off[q + 1] = a.cb_off[q] + wts->codebook_sizes[q];
+  }
+  hipStream_t s = (hipStream_t)stream;
+  ECHO_DISPATCH(dtype,
+      hipLaunchKernelGGL(rvq_encode_kernel<bf16_t>, dim3(rows), dim3(256), 0, s, (const bf16_t*)z, ldz, a, codes, T,
+                         (bf16_t*)zq, ldq, comps, mean, scale, lat, npca),
+      hipLaunchKernelGGL(rvq_encode_kernel<float>, dim3(rows), dim3(256), 0, s, (const float*)z, ldz, a, codes, T,
+                         (float*)zq, ldq, comps, mean, scale, lat, npca));
   ECHO_LAUNCH_CHECK();
   return 0;
 }

@@ -14,8 +14,10 @@ KV caches shared by the three CFG branches, AdaLN table per schedule, the
 40-step loop captured as a hipGraph. Any other model object that exposes the
 reference's duck-typed surface (model.py:563-642) runs through the generic
 loop below, which is the reference loop itself.
-The autoencoder glue (ae_*, speaker latents, crop) is host code around an
-injected `fish_ae`; the autoencoder is outside this repository's scope.
+The autoencoder glue (ae_*, speaker latents, crop) is the reference's host code
+around an injected `fish_ae`; with a `codec.FishAE` (the HIP Fish-S1-DAC, SURVEY
+§8(f) rows 3-4) it dispatches to that object's fused ae_encode / ae_decode /
+batched get_speaker_latent_and_mask.
 """
 from __future__ import annotations
 
@@ -78,9 +80,16 @@ def get_text_input_ids_and_mask(text_arr: List[str], max_length: Optional[int], 
 
 # ---------------------------------------------------------------------------- autoencoder glue (host)
 
+def _fused_ae(fish_ae) -> bool:
+    from .codec import FishAE
+    return isinstance(fish_ae, FishAE)
+
+
 @torch.inference_mode()
 def ae_encode(fish_ae, pca_state: PCAState, audio: torch.Tensor) -> torch.Tensor:
     assert audio.ndim == 3 and audio.shape[1] == 1
+    if _fused_ae(fish_ae):
+        return fish_ae.ae_encode(pca_state, audio)
     z = fish_ae.encode_zq(audio).float()
     z = (z.transpose(1, 2) - pca_state.pca_mean) @ pca_state.pca_components.T
     return z * pca_state.latent_scale
@@ -88,6 +97,8 @@ def ae_encode(fish_ae, pca_state: PCAState, audio: torch.Tensor) -> torch.Tensor
 
 @torch.inference_mode()
 def ae_decode(fish_ae, pca_state: PCAState, z_q: torch.Tensor) -> torch.Tensor:
+    if _fused_ae(fish_ae):
+        return fish_ae.ae_decode(pca_state, z_q)
     z = (z_q / pca_state.latent_scale) @ pca_state.pca_components + pca_state.pca_mean
     return fish_ae.decode_zq(z.transpose(1, 2).to(fish_ae.dtype)).float()
 
@@ -99,6 +110,10 @@ def get_speaker_latent_and_mask(fish_ae, pca_state: PCAState, audio: torch.Tenso
     """Chunked AE encode -> speaker latents + prefix mask (inference.py:250-309)."""
     down = 2048
     assert audio.ndim == 2 and audio.shape[0] == 1
+    if _fused_ae(fish_ae):
+        return fish_ae.get_speaker_latent_and_mask(
+            pca_state, audio, max_speaker_latent_length=max_speaker_latent_length, audio_chunk_size=audio_chunk_size,
+            pad_to_max=pad_to_max, divis_by_patch_size=divis_by_patch_size)
     audio = audio[:, :max_speaker_latent_length * down]
     parts = []
     for i in range(0, audio.shape[1], audio_chunk_size):

@@ -215,7 +215,7 @@ int echo_rope_pairs(int32_t dtype, void* x, int64_t ld, int32_t rows, int32_t he
                     const void* table_bf16, int32_t seq_len, void* stream);
 /* Window-limited causal attention (autoencoder.py:663-706,762-773): qkv [batch*T][3*heads*64]
  * (q | k | v, row stride ld), out [batch*T][heads*64]; query t sees keys max(0,t-window+1)..t.
- * head_dim == 64, window <= 128. */
+ * head_dim == 64, any window (128 for pre/post_module, 512 for the encoder transformer). */
 int echo_window_attention(int32_t dtype, const void* qkv, int64_t ld, void* out, int64_t ldo, int32_t batch,
                           int32_t T, int32_t heads, int32_t head_dim, int32_t window, void* stream);
 /* Decoder tail (autoencoder.py:995-996 + .float()): y[t] = tanh(conv_k7(s)[t] + bias) on the
@@ -225,6 +225,36 @@ int echo_conv_out_tanh(int32_t dtype, const void* s, int64_t lds, int64_t ss, co
 /* find_flattening_point (inference.py:315-330) of x [L][D] fp32 -> *out (device int32). */
 int echo_flattening_point(const float* x, int32_t L, int32_t D, int32_t window, float std_threshold, float target,
                           int32_t* out, void* stream);
+
+/* ---- Fish-S1-DAC input path (csrc/codec.hip). */
+
+/* Encoder input conv (autoencoder.py:913, CausalWNConv1d(1, C, 7)): x [batch][L] audio (dtype,
+ * per-item stride sx) -> y rows [batch][L][C] (row stride ldy, item stride sy). */
+int echo_conv_in(int32_t dtype, const void* x, int64_t sx, const void* w, const void* bias, void* y, int64_t ldy,
+                 int64_t sy, int32_t L, int32_t C, int32_t batch, void* stream);
+
+/* Residual-VQ weights in dtype, weight norm folded: stage 0 = semantic quantizer, 1.. = residual
+ * quantizers (autoencoder.py:376-427). codebook_sizes[q] entries per stage, tables concatenated. */
+typedef struct EchoRvqWeights {
+  const void* w_in;    /* [nq][codebook_dim][D]  in_proj (WN conv k1) */
+  const void* b_in;    /* [nq][codebook_dim] */
+  const void* cbn;     /* F.normalize(codebook) rows, [sum sizes][codebook_dim] */
+  const void* csq;     /* cbn.pow(2).sum(1) as the reference rounds it, [sum sizes] */
+  const void* cb;      /* raw codebook rows (embedding lookup), [sum sizes][codebook_dim] */
+  const void* w_out;   /* [nq][D][codebook_dim]  out_proj (WN conv k1) */
+  const void* b_out;   /* [nq][D] */
+  int32_t codebook_sizes[16];
+  int32_t nq;
+  int32_t codebook_dim; /* 8 */
+} EchoRvqWeights;
+
+/* DownsampleResidualVectorQuantize code path + DAC.encode_zq + ae_encode's PCA projection
+ * (autoencoder.py:451-471,130-157,1117-1126; inference.py:223-229), one workgroup per frame:
+ * z [rows][D] (pre_module output, rows = batch*T, D == 1024) -> codes [batch][nq][T] int32,
+ * zq [rows][D] (dtype, optional: NULL), lat [rows][npca] fp32 = ((zq - mean) @ comps^T) * scale. */
+int echo_rvq_encode(int32_t dtype, const void* z, int64_t ldz, int32_t rows, int32_t T, int32_t D,
+                    const EchoRvqWeights* w, int32_t* codes, void* zq, int64_t ldq, const float* comps,
+                    const float* mean, float scale, float* lat, int32_t npca, void* stream);
 
 /* Library identification (build stamp) — for load checks. */
 const char* echo_version(void);

@@ -11,7 +11,11 @@ as `load_fish_ae_from_hf` does, inference.py:87-99). Per dtype (fp32 = the refer
 bf16 = its FISH_AE_DTYPE option): latents [1, T, 80] -> `ae_decode` (inference.py:232-235), with
 the intermediate tensors of `decode_zq` (autoencoder.py:1129-1132) for localisation.
 Flattening-point cases: `find_flattening_point` (inference.py:315-330) on constructed latents.
-Outputs (data only): ae_<dtype>.safetensors + ae_<dtype>.json, flatten.json.
+Input path, `--encode`: synthetic audio -> `ae_encode` (inference.py:223-229)
+with the codes / z_q / pre_module output of `DAC.encode_zq` (autoencoder.py:1117-1126), and
+`get_speaker_latent_and_mask` (inference.py:250-309) over a multi-chunk clip (fp32); a short clip
+in bf16.
+Outputs (data only): ae_<dtype>.safetensors + ae_<dtype>.json, flatten.json, ae_enc_<dtype>.*.
 """
 from __future__ import annotations
 
@@ -55,11 +59,14 @@ def build_ref(ref_ae, dtype):
     n_dec = sum(1 for k in ref_sd if k.startswith(("decoder.", "quantizer.post_module.", "quantizer.upsample.")))
     assert n_dec == len(shapes) + 2, (n_dec, len(shapes))  # + the two post_module buffers
     state = CW.synthetic_decode_state(dtype=dtype, with_buffers=True)
-    # encoder / codebook parameters are never run on the decode path, but DAC.dtype reads the
-    # FIRST parameter (an encoder bias): give them uninitialised storage of the model dtype
+    state.update(CW.synthetic_encode_state(dtype=dtype))
+    # the encoder / pre_module rope tables and masks, exactly as the reference builds them
     for k, v in ref_sd.items():
         if k not in state:
-            state[k] = torch.empty(v.shape, dtype=v.dtype if v.dtype == torch.bool else dtype)
+            assert k.endswith(("freqs_cis", "causal_mask")), k
+            n = v.shape[0]
+            state[k] = (CW.rope_table(n) if k.endswith("freqs_cis")
+                        else torch.tril(torch.ones(n, n, dtype=torch.bool)))
     dac.load_state_dict(state, strict=True, assign=True)
     return dac.eval()
 
@@ -123,9 +130,60 @@ def gen_flatten(ref_inf):
     print("flatten", [(c["name"], c["point"]) for c in cases])
 
 
+def synthetic_audio(n: int, seed: int) -> torch.Tensor:
+    """[1, n] fp32 in [-1, 1]: three seeded sinusoids with a slow amplitude envelope plus noise."""
+    g = torch.Generator().manual_seed(seed)
+    t = torch.arange(n, dtype=torch.float64) / 44100.0
+    f = 80.0 + 400.0 * torch.rand(3, generator=g, dtype=torch.float64)
+    env = 0.5 + 0.5 * torch.sin(2 * torch.pi * 0.7 * t)
+    x = sum(0.2 * torch.sin(2 * torch.pi * fi * t) for fi in f) * env
+    x = x + 0.02 * torch.randn(n, generator=g, dtype=torch.float64)
+    return x.float().clamp(-1, 1).unsqueeze(0)
+
+
+def gen_encode(ref_ae, ref_inf, dtype, n_stage: int, n_clip: int, chunk: int):
+    """ae_encode on the first n_stage samples with the DAC's stage outputs, and
+    get_speaker_latent_and_mask on n_clip samples in chunks of `chunk` (0: skip)."""
+    name = {torch.float32: "fp32", torch.bfloat16: "bf16"}[dtype]
+    t0 = time.time()
+    dac = build_ref(ref_ae, dtype)
+    comps, mean, scale = CW.synthetic_pca_state()
+    pca = ref_inf.PCAState(pca_components=comps, pca_mean=mean, latent_scale=scale)
+    audio = synthetic_audio(max(n_stage, n_clip), seed=11)
+    out = {"audio": audio}
+    with torch.inference_mode():
+        a = audio[:, :n_stage].unsqueeze(0).to(dtype)
+        z = dac.encoder(a)
+        out["encoder"] = z.float()
+        q = dac.quantizer
+        for j, ds in enumerate(q.downsample):
+            z = ds(z)
+            out[f"downsample_{j}"] = z.float()
+        out["pre_module"] = q.pre_module(z).float()
+        codes, _ = dac.encode(a)
+        out["codes"] = codes
+        out["z_q"] = dac.encode_zq(a).float()
+        lat = ref_inf.ae_encode(dac, pca, a)
+        out["latents"] = lat
+        if n_clip:
+            sl, sm = ref_inf.get_speaker_latent_and_mask(dac, pca, audio[:, :n_clip].to(dtype), audio_chunk_size=chunk)
+            out["speaker_latent"], out["speaker_mask"] = sl.float(), sm
+    save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(HERE, f"ae_enc_{name}.safetensors"))
+    meta = {"dtype": name, "n_stage": n_stage, "n_clip": n_clip, "chunk": chunk, "latent_scale": scale,
+            "codes_shape": list(out["codes"].shape), "seconds": round(time.time() - t0, 1)}
+    with open(os.path.join(HERE, f"ae_enc_{name}.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print(name, meta, flush=True)
+
+
 def main():
     ref_ae, ref_inf = _import_reference()
     torch.set_num_threads(max(1, os.cpu_count() or 1))
+    if "--encode" in sys.argv:
+        # fp32: encoder transformer T = 640 > its window 512, pre_module T = 160 > 128; 2 chunks
+        gen_encode(ref_ae, ref_inf, torch.float32, n_stage=160 * 2048, n_clip=400000, chunk=160 * 2048)
+        gen_encode(ref_ae, ref_inf, torch.bfloat16, n_stage=16 * 2048, n_clip=0, chunk=0)
+        return
     gen_flatten(ref_inf)
     gen(ref_ae, ref_inf, torch.float32, T=6)
     gen(ref_ae, ref_inf, torch.bfloat16, T=6)

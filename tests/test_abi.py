@@ -51,6 +51,7 @@ STRUCTS = {
     "EchoKVSegment": L.KVSegment,
     "EchoAttnArgs": L.AttnArgs,
     "EchoStepArgs": L.StepArgs,
+    "EchoRvqWeights": L.RvqWeights,
 }
 
 
