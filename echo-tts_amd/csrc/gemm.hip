@@ -1010,6 +1010,120 @@ gemm_f32_kernel(const float* __restrict__ A, int64_t lda, int64_t sA,
   }
 }
 
+// fp32 on the f32-input MFMA (v_mfma_f32_32x32x2_f32, exact f32 at the vector rate): 128x128x32
+// tiles, 4 waves of 64x64 (2x2 MFMA tiles). The MFMA result is a k-ordered fmaf chain (one rounding
+// per product, MI355X guide §3), i.e. the same arithmetic as gemm_f32_kernel's per-thread fmaf loop:
+// both kernels are bitwise equal (tested), this one at ~3x the throughput. Operands staged k-major in
+// LDS (A[k][m], W[k][n]) so a lane's fragment element (row l&31, k l>>5) is one conflict-free read;
+// the next K-tile is prefetched into registers during the current tile's MFMAs. The epilogue
+// (bias, SiLU/GELU/Snake, /out_div, SwiGLU, gated residual) is gemm_f32_kernel's on a 128x128 tile.
+constexpr int QM = 128, QN = 128, QK = 32, QP = 4;
+constexpr int Q_LDS = (2 * QK * (QM + QP) > QM * (QN + 1)) ? 2 * QK * (QM + QP) : QM * (QN + 1);
+
+__global__ void __launch_bounds__(256)
+gemm_f32_mfma_kernel(const float* __restrict__ A, int64_t lda, int64_t sA,
+                     const float* __restrict__ W, int64_t ldw, int64_t sW,
+                     void* __restrict__ Cv, int64_t ldc, int64_t sC, int M, int N, int K, Epi ep) {
+  __shared__ __attribute__((aligned(16))) float sm[Q_LDS];
+  float(*As)[QM + QP] = (float(*)[QM + QP])sm;
+  float(*Ws)[QN + QP] = (float(*)[QN + QP])(sm + QK * (QM + QP));
+  const int z = blockIdx.z;
+  A += z * sA;
+  W += z * sW;
+  const int m0 = blockIdx.y * QM, n0 = blockIdx.x * QN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  f32x4 ra[4], rw[4];
+  auto gload = [&](int k0) {
+    const int64_t td = tap_delta(ep, k0, lda);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i, r = e >> 3, c = e & 7;
+      ra[i] = *(const f32x4*)(A + (int64_t)min(m0 + r, M - 1) * lda + k0 + c * 4 + td);
+      rw[i] = *(const f32x4*)(W + (int64_t)min(n0 + r, N - 1) * ldw + k0 + c * 4);
+    }
+  };
+  gload(0);
+  for (int k0 = 0; k0 < K; k0 += QK) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i, r = e >> 3, c = e & 7;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        As[c * 4 + j][r] = ra[i][j];
+        Ws[c * 4 + j][r] = rw[i][j];
+      }
+    }
+    __syncthreads();
+    if (k0 + QK < K) gload(k0 + QK);
+#pragma unroll
+    for (int kk = 0; kk < QK / 2; ++kk) {
+      const int kr = kk * 2 + (lane >> 5), li = lane & 31;
+      const float a0 = As[kr][wm * 64 + li], a1 = As[kr][wm * 64 + 32 + li];
+      const float b0 = Ws[kr][wn * 64 + li], b1 = Ws[kr][wn * 64 + 32 + li];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  float(*Ct)[QN + 1] = (float(*)[QN + 1])sm;
+  const float* bias = ep.bias ? (const float*)ep.bias + z * ep.stride_bias : nullptr;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int r = wm * 64 + i * 32 + (g & 3) + 8 * (g >> 2) + 4 * (lane >> 5);
+        const int cc = wn * 64 + j * 32 + (lane & 31);
+        const int n = n0 + cc;
+        float v = acc[i][j][g];
+        if (bias && ep.epi != ECHO_EPI_SWIGLU) v += bias[min(n, N - 1)];
+        if (ep.act == ECHO_ACT_SILU) v = silu_f(v);
+        else if (ep.act == ECHO_ACT_GELU) v = gelu_erf(v);
+        else if (ep.act == ECHO_ACT_SNAKE) v = snake_f32(v, ((const float*)ep.act_alpha)[min(n, N - 1)]);
+        if (ep.out_div != 0.0f) v = v / ep.out_div;
+        Ct[r][cc] = v;
+      }
+  __syncthreads();
+  if (ep.epi == ECHO_EPI_SWIGLU) {
+    for (int e = tid; e < QM * QN / 2; e += 256) {
+      const int r = e / (QN / 2), o = e % (QN / 2);
+      const int ca = (o / 16) * 32 + (o % 16);
+      const int m = m0 + r, n = n0 / 2 + o;
+      if (m < M && n < N / 2) ((float*)Cv)[z * sC + (int64_t)m * ldc + n] = silu_f(Ct[r][ca]) * Ct[r][ca + 16];
+    }
+    return;
+  }
+  for (int e = tid; e < QM * QN; e += 256) {
+    const int r = e / QN, cc = e % QN;
+    const int m = m0 + r, n = n0 + cc;
+    if (m >= M || n >= N) continue;
+    float v = Ct[r][cc];
+    if (ep.epi == ECHO_EPI_RESID) {
+      if (ep.gate) v = ((const float*)ep.gate)[z * ep.stride_gate + n] * v;
+      v = ((const float*)ep.aux)[z * ep.stride_aux + (int64_t)m * ep.ld_aux + n] + v;
+    }
+    ((float*)Cv)[z * sC + (int64_t)m * ldc + n] = v;
+  }
+}
+
+// the MFMA kernel reads 16-B rows chunks: 16-B aligned operands, K-tiles that never straddle a conv tap
+bool f32_mfma_ok(const EchoGemmArgs* a) {
+  if (a->tile == 19) return false;  // diagnostic: force the scalar fp32 kernel
+  if (((uintptr_t)a->A | (uintptr_t)a->W) & 15) return false;
+  if (a->lda % 4 || a->ldw % 4 || a->stride_a % 4 || a->stride_w % 4 || a->K % QK) return false;
+  if (a->conv_taps > 0 && a->conv_c % QK) return false;
+  return true;
+}
+
 struct TileCfg { int bm, bn, occ; float eff; };
 constexpr TileCfg kTiles[] = {  // eff: per-tile throughput relative to the 2-phase ping-pong 256x256
     {256, 256, 1, 1.00f},  // 1: 8 waves, 128x64 per wave (runs gemm_bf16_pp2_kernel)
@@ -1223,6 +1337,14 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
     return echo_head_norm_rope(a->dtype, a->C, a->ldc, a->M, a->hn_heads, a->hn_nblk, 0,
                                (int64_t)a->hn_heads * 128, a->hn_w, a->hn_w_stride, a->hn_rope, a->hn_rope_heads,
                                a->hn_seq_len, a->hn_pos0, a->hn_pos_mult, a->hn_eps, stream);
+  }
+  if (a->dtype == ECHO_F32 && f32_mfma_ok(a)) {
+    dim3 grid((a->N + QN - 1) / QN, (a->M + QM - 1) / QM, a->batch);
+    hipLaunchKernelGGL(gemm_f32_mfma_kernel, grid, dim3(256), 0, s, (const float*)a->A, a->lda, a->stride_a,
+                       (const float*)a->W, a->ldw, a->stride_w, a->C, a->ldc, a->stride_c, a->M, a->N,
+                       a->K, ep);
+    ECHO_LAUNCH_CHECK();
+    return 0;
   }
   if (a->dtype == ECHO_F32) {
     dim3 grid((a->N + FT - 1) / FT, (a->M + FT - 1) / FT, a->batch);

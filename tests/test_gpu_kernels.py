@@ -189,6 +189,49 @@ def test_gemm_f32():
     assert rel(h, ref) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K,kind", [(130, 96, 192, "store"), (1000, 256, 448, "snake"), (257, 128, 64, "gelu"),
+                                         (300, 192, 256, "swiglu"), (513, 128, 128, "resid")])
+def test_gemm_f32_mfma_bitwise_equals_fmaf_chain(M, N, K, kind):
+    """The f32-input MFMA kernel (default fp32 path) vs the scalar fmaf-chain kernel (tile 19):
+    both are k-ordered fmaf chains, so every output is bitwise equal."""
+    a = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV) * 0.1
+    kw = {}
+    if kind in ("store", "snake", "gelu"):
+        kw["bias"] = torch.randn(N, device=DEV)
+    if kind == "snake":
+        kw.update(act=L.ACT_SNAKE, act_alpha=1 + 0.1 * torch.randn(N, device=DEV))
+    if kind == "gelu":
+        kw["act"] = L.ACT_GELU
+    if kind == "swiglu":
+        kw["epilogue"] = L.EPI_SWIGLU
+    outs = []
+    for tile in (0, 19):
+        if kind == "resid":
+            h = torch.randn(M, N, device=DEV, generator=torch.Generator(DEV).manual_seed(3))
+            g = torch.randn(N, device=DEV, generator=torch.Generator(DEV).manual_seed(4))
+            ops.gemm(a, w, out=h, epilogue=L.EPI_RESID, aux=h, gate=g, tile=tile)
+            outs.append(h)
+        else:
+            outs.append(ops.gemm(a, w, tile=tile, **kw))
+    assert torch.equal(outs[0], outs[1])
+    if kind == "store":
+        assert rel(outs[0], ref_linear(a, w, kw["bias"])) < 1e-5
+
+
+def test_gemm_f32_mfma_conv_bitwise():
+    """Causal conv GEMM (taps 7, dilation 3) on the MFMA kernel == scalar kernel, bitwise."""
+    B, Lr, C, N, PADR = 2, 300, 64, 128, 32
+    buf = torch.zeros(B, PADR + Lr, C, device=DEV)
+    buf[:, PADR:] = torch.randn(B, Lr, C, device=DEV)
+    w = torch.randn(N, 7 * C, device=DEV) * 0.05
+    o = [ops.gemm(buf[:, PADR:], w, conv=(7, 3), tile=t) for t in (0, 19)]
+    assert torch.equal(o[0], o[1])
+    x = buf.permute(0, 2, 1).cpu().double()
+    ref = torch.nn.functional.conv1d(x, w.cpu().double().view(N, 7, C).permute(0, 2, 1), dilation=3)
+    assert rel(o[0], ref[..., -Lr:].permute(0, 2, 1)) < 1e-5
+
+
 def test_gemm_rejects_bad_args():
     a = torch.randn(16, 100, device=DEV).to(BF)
     w = torch.randn(32, 100, device=DEV).to(BF)
