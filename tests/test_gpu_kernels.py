@@ -299,6 +299,54 @@ def test_attention_variants_match_production(variant):
         assert (st[:n, 3] >= st[:n, 0]).all() and (st[:n, 0] > 0).all()
 
 
+@pytest.mark.parametrize("variant", [8, 9])
+@pytest.mark.parametrize("n,H", [(200, 4), (640, 16), (1, 2), (129, 2)])
+def test_attention_paired_head_variant_bitwise(variant, n, H):
+    """Paired-head 8-wave kernel (two heads per workgroup, staggered wave groups): the same tile
+    math and softmax order as the production kernel, so bitwise equal, on the decoder's segment
+    layout [self | text (per-row lengths incl. 0) | speaker (per-row lengths incl. 0)]."""
+    B = 2
+    R = 3 * B
+    qkvg = torch.randn(R, n, 4, H, 128, device=DEV).to(BF)
+    kt = torch.randn(B, 200, 2, H, 128, device=DEV).to(BF)
+    ks = torch.randn(B, 80, 2, H, 128, device=DEV).to(BF)
+    tl = torch.tensor([50, 200, 0, 0, 50, 200], dtype=torch.int32, device=DEV)
+    sl = torch.tensor([80, 17, 80, 17, 0, 0], dtype=torch.int32, device=DEV)
+    segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2]),
+            ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=B),
+            ops.Segment(ks[:, :, 0], ks[:, :, 1], lens=sl, batch_mod=B)]
+    ref = torch.empty(R, n, H, 128, device=DEV, dtype=BF)
+    ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
+    got = torch.full_like(ref, float("nan"))
+    ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=variant)
+    assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("variant", [8, 9])
+def test_attention_engine_kv_layout(variant):
+    """The engine's KV layout: one [B, T, 24, 2, H, 128] buffer per stream, layer = strided view
+    (1.4 GB for B=16, T=448): tile base addresses span > 2^31 bytes, so any 32-bit address word
+    handled as signed shows up here. Bitwise against the production kernel."""
+    B, N, H, T, P = 16, 640, 16, 448, 160
+    R = 3 * B
+    qkvg = torch.randn(R, N, 4, H, 128, device=DEV).to(BF)
+    kt = torch.empty(B, T, 24, 2, H, 128, device=DEV, dtype=BF)
+    ks = torch.empty(B, P, 24, 2, H, 128, device=DEV, dtype=BF)
+    kt[:, :, 23].normal_()
+    ks[:, :, 23].normal_()
+    tl = torch.tensor([388] * B + [0] * B + [388] * B, dtype=torch.int32, device=DEV)
+    sl = torch.tensor([160] * 2 * B + [0] * B, dtype=torch.int32, device=DEV)
+    segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2]),
+            ops.Segment(kt[:, :, 23, 0], kt[:, :, 23, 1], lens=tl, batch_mod=B),
+            ops.Segment(ks[:, :, 23, 0], ks[:, :, 23, 1], lens=sl, batch_mod=B)]
+    ref = torch.empty(R, N, H, 128, device=DEV, dtype=BF)
+    ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
+    got = torch.full_like(ref, float("nan"))
+    ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=variant)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
 @pytest.mark.parametrize("variant", [5])
 @pytest.mark.parametrize("n", [1, 63, 200, 333])
 def test_attention_variant_causal_segments(variant, n):
