@@ -25,6 +25,13 @@ namespace {
 
 __device__ __forceinline__ int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
+// max of three fp32 values in one v_max3_f32 (scores are finite or -inf: no NaN handling needed)
+__device__ __forceinline__ float max3_f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 __device__ __forceinline__ int remap_xcd(int bid, int nwg) {
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
@@ -278,7 +285,9 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
   int cur = 0;
   if (ABL & 64) ntiles = 0;
   uint64_t* ph = ((ABL & 512) && blockIdx.x == 0) ? g_attn_stamps + (int64_t)gridDim.x * 6 + w * 64 * 6 : nullptr;
-  for (int ti = 0; ti < ntiles; ++ti) {
+  // one tile; `cur` (the LDS buffer of tile ti) is a literal in the 2-buffer schedules, so every
+  // fragment address is a per-lane base + an immediate offset (no per-tile address arithmetic)
+  auto tile_body = [&](int ti, int cur) __attribute__((always_inline)) {
     if ((ABL & 512) && ph && ti < 64) phase_stamp(ph + ti * 6 + 0);
     if constexpr (ST == 0) {
       // buffer cur^1 held tile ti-1: every wave passed the barrier after reading it
@@ -345,12 +354,30 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
         }
     }
 #pragma unroll
-    for (int kk = 0; kk < NKK; ++kk)
+    for (int kk = 0; kk < NKK; ++kk) {
+      // v_max3 chain: hipcc's fmaxf first canonicalises every MFMA output (one v_max each)
+      float m = max3_f(st[kk][0], st[kk][1], st[kk][2]);
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) mx = fmaxf(mx, fmaxf(st[kk][r], st[kk][r + 1]));
+      for (int r = 3; r < 15; r += 2) m = max3_f(m, st[kk][r], st[kk][r + 1]);
+      mx = max3_f(mx, m, st[kk][15]);
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float msc = m_new == -INFINITY ? 0.f : -m_new * sl2;
+    // deferred running max (cdna_hip_programming.md T13): the max moves only when some lane's
+    // tile max exceeds it by more than 8 in exp2 units, so P <= 2^8 (fp32 O and l have the
+    // range, a bf16 P the same relative precision) and the O rescale runs on a few tiles instead
+    // of nearly every tile; it is applied before this tile's P is formed (textbook order)
+    if (__any(m_run == -INFINITY || (mx - m_run) * sl2 > 8.0f)) {
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha =
+          __builtin_amdgcn_exp2f(__builtin_fmaf(m_run, sl2, m_new == -INFINITY ? 0.f : -m_new * sl2));
+      l_run *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+      m_run = m_new;
+    }
+    const float msc = m_run == -INFINITY ? 0.f : -m_run * sl2;
     float psum = 0.f;
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk)
@@ -360,16 +387,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
         st[kk][r] = pv;
         psum += pv;
       }
-    if (__any(m_new != m_run)) {  // otherwise alpha == 1 exactly for every lane
-      const float alpha = __builtin_amdgcn_exp2f(__builtin_fmaf(m_run, sl2, msc));
-      l_run *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-    }
     l_run += psum;
-    m_run = m_new;
     }
     if ((ABL & 512) && ph && ti < 64) phase_stamp(ph + ti * 6 + 2);
 
@@ -418,7 +436,6 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
     if ((ABL & 512) && ph && ti < 64) phase_stamp(ph + ti * 6 + 3);
     if constexpr (ST == 0) {
       __syncthreads();  // tile ti+1 was written at the top of this tile
-      cur ^= 1;
     } else {
       // tile ti+1 landed (this wave's share; later tiles may stay in flight) ... and everyone's
       if (ST == 3 && ti + 2 < ntiles && !(ABL & 1)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPT) : "memory");
@@ -426,7 +443,18 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
       if ((ABL & 512) && ph && ti < 64) phase_stamp(ph + ti * 6 + 4);
       __syncthreads();
       if ((ABL & 512) && ph && ti < 64) phase_stamp(ph + ti * 6 + 5);
+    }
+  };
+  if constexpr (ST == 3) {
+    for (int ti = 0; ti < ntiles; ++ti) {
+      tile_body(ti, cur);
       cur = cur == ST - 1 ? 0 : cur + 1;
+    }
+  } else {
+    for (int ti = 0; ti < ntiles; ti += 2) {
+      tile_body(ti, 0);
+      if (ti + 1 >= ntiles) break;
+      tile_body(ti + 1, 1);
     }
   }
 
@@ -694,281 +722,6 @@ __global__ void __launch_bounds__(256, 2) attn_pipe_kernel(EchoAttnArgs a) {
     }
 }
 
-// ----------------------------------------------------------------------------- paired-head, 8 waves
-// One workgroup = 8 waves = two groups of 4: group 0 takes head h, group 1 head h + H/2, both for the
-// same (row, 128-query block), so both groups walk identical tile lists (same masks, same lengths).
-// Wave w and wave w+4 share a SIMD (MI355X_MICROARCH.md "Two waves per SIMD"); the groups run the
-// same per-tile program one barrier interval apart, so on every SIMD one wave is in its matrix
-// segment while its partner is in its VALU segment:
-//   V segment of tile t: mask + online softmax of S(t) (exp2, row sums, bf16 pack of P(t), O rescale),
-//                        LDS-DMA of K(t+2) and V(t+1), wait for K(t+1) and V(t) (this wave's share)
-//   C segment of tile t: S(t+1) = K(t+1).Q^T (16 MFMA)  +  O^T += V(t)^T.P(t) (16 MFMA)
-// with one workgroup barrier after each segment. Group 1 runs one interval late (one extra barrier
-// before its first QK^T), group 0 stores its output while group 1 runs its last C segment and then
-// passes one extra barrier, so both groups execute the same barrier count.
-// K and V have separate 2-slot rings per group: K(t+2) goes to the slot K(t) used (last read in
-// C(t-1)), V(t+1) to the slot of V(t-1) (last read in C(t-1)); every wave passed the barrier after
-// C(t-1) before issuing them. Tile math, LDS image and numerics are those of attn_bf16_kernel.
-// ABL (timing only, results wrong): 1 no loop DMA, 2 no softmax, 4 no PV, 8 no QK, 16 no loop barriers,
-// 64 no tiles (prologue + epilogue), 1024 static priority for waves 4-7 (results exact).
-constexpr int PW_MAXT = 128;  // tiles per row in attn_pw_kernel's LDS tile table
-
-template <int ABL>
-__global__ void __launch_bounds__(512, 1) attn_pw_kernel(EchoAttnArgs a) {
-  constexpr int NW = 4, QB = 128, KTT = 64, DPT = 4;
-  // [group][K slot 0, K slot 1, V slot 0, V slot 1][64 keys x 128]
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 4 * KTT * 128];
-  // flat tile list of the row: {K base, V base (head 0, tile's first key), token stride, last valid row}
-  __shared__ __attribute__((aligned(16))) uint32_t ttab[PW_MAXT * 8];
-
-  const int nqb = (a.n_q + QB - 1) / QB;
-  const int L = remap_xcd(blockIdx.x, gridDim.x);
-  const int qb = L % nqb;
-  const int row = (L / nqb) % a.rows;  // rows fastest (see attn_bf16_kernel)
-  const int hp = L / (nqb * a.rows);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w8 = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = w8 >> 2, w = w8 & 3;
-  const int head_g = hp + grp * (a.heads >> 1);
-  const int h2 = lane >> 5, ql = lane & 31;
-  const int g_ = lane >> 4, q4_ = (lane & 15) >> 2, p4_ = lane & 3;
-  const int q0 = qb * QB;
-  const int qi = q0 + w * 32 + ql;
-  const int qc = min(qi, a.n_q - 1);
-  bf16_t* const glds = lds + grp * 4 * KTT * 128;
-
-  if ((ABL & 1024) && grp == 1) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
-
-  const bf16_t* qp = (const bf16_t*)a.q + row * a.q_ld_batch + (int64_t)qc * a.q_ld_tok + head_g * 128;
-  bf16x8 qf[8];
-#pragma unroll
-  for (int ds = 0; ds < 8; ++ds) qf[ds] = *(const bf16x8*)(qp + 16 * ds + 8 * h2);
-
-  int ntiles_row;
-  {
-    const int head = 0;  // the table holds head-0 bases; each group adds its head offset
-    ECHO_SEG_TABLE()
-    const int n0 = (ke0 + KTT - 1) / KTT, n1 = (ke1 + KTT - 1) / KTT, n2 = (ke2 + KTT - 1) / KTT;
-    const int f1 = n0, f2 = n0 + n1, f3 = n0 + n1 + n2;
-    if (tid < ntiles) {
-      const int sg = (tid >= f1) + (tid >= f2) + (tid >= f3);
-      const int t0 = (tid - sel4(sg, 0, f1, f2, f3)) * KTT;
-      const int64_t ld = sel4(sg, ld0, ld1, ld2, ld3);
-      const bf16_t* kb = sel4(sg, kb0, kb1, kb2, kb3) + t0 * ld;
-      const bf16_t* vb = sel4(sg, vb0, vb1, vb2, vb3) + t0 * ld;
-      const uint64_t ku = (uint64_t)(uintptr_t)kb, vu = (uint64_t)(uintptr_t)vb;
-      *(uint4*)&ttab[tid * 8] = make_uint4((uint32_t)ku, (uint32_t)(ku >> 32), (uint32_t)vu, (uint32_t)(vu >> 32));
-      *(uint2*)&ttab[tid * 8 + 4] = make_uint2((uint32_t)ld, (uint32_t)(sel4(sg, ke0, ke1, ke2, ke3) - 1 - t0));
-    }
-    ntiles_row = ntiles;
-  }
-  int ntiles = ntiles_row;
-  // Q consumed here (one wait for it), table visible to every wave
-#pragma unroll
-  for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));
-  __syncthreads();
-
-  auto entry_base = [&](int t, int part) __attribute__((always_inline)) -> const bf16_t* {
-    const uint2 e = *(const uint2*)&ttab[t * 8 + 2 * part];
-    // readfirstlane returns int: zero-extend the low word (a sign-extended one corrupts the address)
-    const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(e.x) |
-                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(e.y) << 32);
-    return (const bf16_t*)(uintptr_t)u + head_g * 128;
-  };
-  auto entry_ld_last = [&](int t) __attribute__((always_inline)) -> int2 {
-    const uint2 e = *(const uint2*)&ttab[t * 8 + 4];
-    return make_int2(__builtin_amdgcn_readfirstlane(e.x), __builtin_amdgcn_readfirstlane(e.y));
-  };
-
-  const int dr = lane >> 4, dp = lane & 15;
-  // K (part 0) or V (part 1) of tile t into `slot`: 16 wave-instructions of 1 KiB per group
-  auto dma_part = [&](int t, int part, int slot) __attribute__((always_inline)) {
-    const bf16_t* base = entry_base(t, part);
-    const int2 ll = entry_ld_last(t);
-#pragma unroll
-    for (int i = 0; i < DPT; ++i) {
-      const int r = (i * NW + w) * 4 + dr;
-      const uint32_t voff = (uint32_t)(min(r, ll.y) * ll.x + ((dp ^ swz(r)) * 8)) * 2u;
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(
-          lds_addr_of(glds + (part * 2 + slot) * KTT * 128 + ((i * NW + w) * 4) * 128));
-      glds16s(base, voff, dst);
-    }
-  };
-  // workgroup barrier that the scheduler may not move instructions across
-  auto barrier = []() __attribute__((always_inline)) {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  // per-lane LDS byte offsets of the fragment reads (group base included); tile slot, 32-key half
-  // (kk) and 16-key quarter (s2) are immediates: swz() of rows r + 16 s2 + 32 kk equals swz(r)
-  const char* const lbytes = (const char*)lds;
-  uint32_t kofs[8], vofs[8];
-#pragma unroll
-  for (int ds = 0; ds < 8; ++ds)
-    kofs[ds] = grp * 4 * KTT * 256 + (ql * 128 + (((2 * ds + h2) ^ swz(ql)) * 8)) * 2;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    const int ch = 4 * dt + 2 * (g_ & 1) + (p4_ >> 1);
-    const int r0 = 4 * h2 + q4_, r1 = r0 + 8;
-    vofs[2 * dt] = grp * 4 * KTT * 256 + (r0 * 128 + ((ch ^ swz(r0)) * 8) + (p4_ & 1) * 4) * 2;
-    vofs[2 * dt + 1] = grp * 4 * KTT * 256 + (r1 * 128 + ((ch ^ swz(r1)) * 8) + (p4_ & 1) * 4) * 2;
-  }
-  auto qk_tile = [&](auto SLOT, f32x16 (&st)[2]) __attribute__((always_inline)) {
-    constexpr int sb = decltype(SLOT)::value * KTT * 256;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) st[kk][r] = 0.f;
-#pragma unroll
-      for (int ds = 0; ds < 8; ++ds) {
-        const bf16x8 kf = *(const bf16x8*)(lbytes + kofs[ds] + (sb + kk * 32 * 256));
-        st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], st[kk], 0, 0, 0);
-      }
-    }
-  };
-
-  f32x16 o[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
-  const float sl2 = a.scale * 1.4426950408889634f;
-
-  // one tile: V segment (softmax of sc = S(t)), barrier, C segment (QK(t+1) -> sn, PV(t)), barrier
-  auto iter = [&](auto PAR, int t, f32x16 (&sc)[2], f32x16 (&sn)[2]) __attribute__((always_inline)) {
-    constexpr int P = decltype(PAR)::value;  // t & 1
-    // ---- V segment
-    bf16x8 pf[4];
-    if (ABL & 2) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) pf[i] = qf[i];
-    } else {
-      const int last = entry_ld_last(t).y;
-      if (last < KTT - 1) {  // partial tile: keys past the segment's valid length
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
-            sc[kk][r] = key <= last ? sc[kk][r] : -INFINITY;
-          }
-      }
-      float m0 = -INFINITY, m1 = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        m0 = fmaxf(m0, fmaxf(sc[0][r], sc[0][r + 1]));
-        m1 = fmaxf(m1, fmaxf(sc[1][r], sc[1][r + 1]));
-      }
-      const float mx = fmaxf(m0, m1);
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      const float m_new = fmaxf(m_run, fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])));
-      const float msc = m_new == -INFINITY ? 0.f : -m_new * sl2;
-      if (__any(m_new != m_run)) {  // otherwise alpha == 1 exactly for every lane
-        const float alpha = __builtin_amdgcn_exp2f(__builtin_fmaf(m_run, sl2, msc));
-        l_run *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-      }
-      m_run = m_new;
-      float psum = 0.f;  // summed in attn_bf16_kernel's order (bitwise-equal results)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kk][8 * s2 + j], sl2, msc));
-            psum += pv;
-            pf[kk * 2 + s2][j] = (__bf16)pv;
-          }
-      l_run += psum;
-    }
-    // pin the softmax (P) inside the V segment: without this, IR-level sinking moves the
-    // exp2 chain next to its only consumers, the PV MFMAs of the C segment
-    asm volatile("" : "+v"(pf[0]), "+v"(pf[1]), "+v"(pf[2]), "+v"(pf[3]));
-    const bool k2 = t + 2 < ntiles, v1 = t + 1 < ntiles;
-    if (!(ABL & 1)) {
-      if (k2) dma_part(t + 2, 0, P);       // K(t+2) into the slot of K(t)
-      if (v1) dma_part(t + 1, 1, P ^ 1);   // V(t+1) into the slot of V(t-1)
-      // K(t+1) and V(t) landed (this wave's share); the DMA just issued may stay in flight
-      if (k2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (v1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    if (!(ABL & 16)) barrier();
-    // ---- C segment
-    if (v1 && !(ABL & 8)) {
-      qk_tile(std::integral_constant<int, P ^ 1>{}, sn);
-      // K fragment reads 4 MFMAs ahead
-      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (k < 12) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < ((ABL & 4) ? 0 : 2); ++kk)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        constexpr int vb = (2 + P) * KTT * 256;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const int im = vb + (kk * 32 + 16 * s2) * 256;
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(lbytes + vofs[2 * dt] + im));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(lbytes + vofs[2 * dt + 1] + im));
-          typedef __attribute__((ext_vector_type(8))) short s16x8;
-          const s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf[kk * 2 + s2], o[dt],
-                                                           0, 0, 0);
-        }
-      }
-    // V^T transposed reads (2 per MFMA) 2 MFMAs ahead
-    if (!(ABL & 4)) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 4, 1);
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-        if (k < 14) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-      }
-    }
-    if (!(ABL & 16)) barrier();
-  };
-
-  // prologue: K(0), V(0), K(1) in flight; K(0) and V(0) landed
-  if (ntiles > 0) { dma_part(0, 0, 0); dma_part(0, 1, 0); }
-  if (ntiles > 1) { dma_part(1, 0, 1); asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  barrier();
-  if (grp == 1) barrier();  // stagger: group 1 runs one interval behind group 0
-  f32x16 sa[2], sb[2];
-  if (ABL & 64) ntiles = 0;
-  if (ntiles > 0) qk_tile(std::integral_constant<int, 0>{}, sa);
-  barrier();
-  for (int t = 0; t < ntiles; t += 2) {
-    iter(std::integral_constant<int, 0>{}, t, sa, sb);
-    if (t + 1 >= ntiles) break;
-    iter(std::integral_constant<int, 1>{}, t + 1, sb, sa);
-  }
-
-  // ---- epilogue: normalise, round, gate, store
-  const auto lsw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
-  const float inv = 1.0f / (__uint_as_float(lsw[0]) + __uint_as_float(lsw[1]));
-  {
-    bf16_t* op = (bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qc * a.o_ld_tok + head_g * 128;
-    const bf16_t* gp = a.gate ? (const bf16_t*)a.gate + row * a.g_ld_batch + (int64_t)qc * a.g_ld_tok + head_g * 128
-                              : nullptr;
-    attn_store_out(o, inv, qi, h2, qi < a.n_q, op, gp);
-  }
-  if (grp == 0) barrier();  // matches group 1's stagger barrier; group 1's last C segment runs meanwhile
-}
-
 // ----------------------------------------------------------------------------- fp32 (parity mode)
 constexpr int FQ = 64, FKT = 32;
 
@@ -1058,19 +811,6 @@ int check_attn_args(const EchoAttnArgs* a) {
   return 0;
 }
 
-bool has_causal(const EchoAttnArgs* a) {
-  for (int s = 0; s < a->nseg; ++s)
-    if (a->seg[s].k && a->seg[s].causal) return true;
-  return false;
-}
-
-int total_tiles(const EchoAttnArgs* a, int kt) {  // upper bound: segment capacities
-  int n = 0;
-  for (int s = 0; s < a->nseg; ++s)
-    if (a->seg[s].k) n += (a->seg[s].capacity + kt - 1) / kt;
-  return n;
-}
-
 int attn_grid(const EchoAttnArgs* a, int qb) { return ((a->n_q + qb - 1) / qb) * a->heads * a->rows; }
 
 // Measurement variants of the bf16 kernel (tools/bench_attn.py; DESIGN.md §7 lists what each
@@ -1113,19 +853,6 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       else if (abl == 0) hipLaunchKernelGGL((attn_pipe_kernel<0>), grid, dim3(256), 0, s, *a);
       else return ECHO_EINVAL;
       break;
-    case 8:
-    case 9: {  // paired-head 8-wave kernel (9: static priority for waves 4-7)
-      if ((a->heads & 1) || has_causal(a) || total_tiles(a, 64) > PW_MAXT) return ECHO_EINVAL;
-      const dim3 g2(attn_grid(a, 128) / 2);
-      switch (abl + (cfg == 9 ? 1024 : 0)) {
-#define ECHO_PW(A) case A: hipLaunchKernelGGL((attn_pw_kernel<A>), g2, dim3(512), 0, s, *a); break;
-        ECHO_PW(0) ECHO_PW(1) ECHO_PW(2) ECHO_PW(4) ECHO_PW(8) ECHO_PW(12) ECHO_PW(14) ECHO_PW(15) ECHO_PW(16)
-        ECHO_PW(17) ECHO_PW(64) ECHO_PW(1024)
-#undef ECHO_PW
-        default: return ECHO_EINVAL;
-      }
-      break;
-    }
     case 6: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 2, 32); break;
     case 7: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 3, 32); break;
     default: return ECHO_EINVAL;
