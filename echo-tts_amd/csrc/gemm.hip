@@ -1162,7 +1162,10 @@ int split_rows(int M, int N, int* tail_cfg) {
   if (M1 == 0 || M1 >= M) return 0;
   const double full = tile_cost(0, M, N, 1);
   double best = 1e300;
-  for (int c = 1; c < 5; ++c) {
+  // tail candidates: the multi-block-per-CU configs. 256x128 (config 2) leaves half the CUs idle on
+  // these tails and measured slowest (M=2048 N=2048, K 2048 / 5888: 37.5 / 85.2 us vs 28.2 / 61.4 us
+  // for 128x64, tools/bench_gemm.py), which the round-based cost model does not see
+  for (int c = 2; c < 5; ++c) {
     const double e = tile_cost(c, M - M1, N, 1);
     if (e < best) { best = e; *tail_cfg = c + 1; }
   }
