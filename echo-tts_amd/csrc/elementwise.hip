@@ -94,6 +94,48 @@ __global__ void __launch_bounds__(NB) adaln_kernel(const T* __restrict__ x, T* _
   }
 }
 
+// Same math for the decoder's shape (bf16, one (shift, scale1) vector for every row, dim = 512*CH):
+// one wave per row, each lane 8*CH columns in 16-B chunks; the lane's slice of the two vectors is
+// loaded once and kept in registers while the wave strides over rows, and the row sum is a wave
+// butterfly (no LDS, no block barrier). Rounding points as adaln_kernel (one bf16 rounding of
+// (x*r)*s1 + shift in fp32); the fp32 sum order differs, so r may differ in its last bit.
+template <int CH>
+__global__ void __launch_bounds__(256) adaln_rows_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                         int rows, const bf16_t* __restrict__ shift,
+                                                         const bf16_t* __restrict__ scale1, float eps) {
+  constexpr int dim = 512 * CH;
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * 4) + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * 4;
+  float s1[CH][8], sh[CH][8];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    load8(scale1 + (c * 64 + lane) * 8, s1[c]);
+    load8(shift + (c * 64 + lane) * 8, sh[c]);
+  }
+  for (int row = wave; row < rows; row += nwaves) {
+    const bf16_t* xr = x + (int64_t)row * dim;
+    bf16_t* yr = y + (int64_t)row * dim;
+    float v[CH][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) load8(xr + (c * 64 + lane) * 8, v[c]);
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += v[c][e] * v[c][e];
+    ss = wave_sum(ss);
+    const float r = 1.0f / sqrtf(ss / (float)dim + eps);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = ((v[c][e] * r) * s1[c][e]) + sh[c][e];
+      store8(yr + (c * 64 + lane) * 8, o);
+    }
+  }
+}
+
 // Per-head RMSNorm (+RoPE) in place: one wave per (row, 4 heads), 16 lanes per head,
 // 8 elements per lane (RoPE pairs are lane-local).
 template <typename T>
@@ -261,6 +303,18 @@ int echo_adaln_modulate(int32_t dtype, const void* x, void* y, int32_t rows, int
                         const void* scale1, int32_t rows_per_vec, int64_t vec_stride, float eps, void* stream) {
   if (!x || !y || !shift || !scale1 || rows <= 0 || dim % 8 || dim > 8 * NB * 4) return ECHO_ESHAPE;
   if (rows_per_vec <= 0) rows_per_vec = rows;
+  if (dtype == ECHO_BF16 && rows_per_vec >= rows && (dim == 1024 || dim == 2048 || dim == 4096)) {
+    // one vector pair for all rows: wave-per-row kernel, <= 8 rows per wave
+    const int blocks = min((rows + 3) / 4, 2048);
+    const hipStream_t st = (hipStream_t)stream;
+    const bf16_t *xb = (const bf16_t*)x, *shb = (const bf16_t*)shift, *s1b = (const bf16_t*)scale1;
+    bf16_t* yb = (bf16_t*)y;
+    if (dim == 1024) hipLaunchKernelGGL(adaln_rows_kernel<2>, dim3(blocks), dim3(256), 0, st, xb, yb, rows, shb, s1b, eps);
+    else if (dim == 2048) hipLaunchKernelGGL(adaln_rows_kernel<4>, dim3(blocks), dim3(256), 0, st, xb, yb, rows, shb, s1b, eps);
+    else hipLaunchKernelGGL(adaln_rows_kernel<8>, dim3(blocks), dim3(256), 0, st, xb, yb, rows, shb, s1b, eps);
+    ECHO_LAUNCH_CHECK();
+    return 0;
+  }
   DISPATCH(dtype, hipLaunchKernelGGL(adaln_kernel<T>, dim3(rows), dim3(NB), 0, (hipStream_t)stream, (const T*)x,
                                      (T*)y, dim, (const T*)shift, (const T*)scale1, rows_per_vec, vec_stride,
                                      eps));

@@ -423,6 +423,20 @@ def test_attention_deferred_max_spikes():
     close_bf16(out, ref)
 
 
+@pytest.mark.parametrize("dim,rows", [(2048, 1), (2048, 9001), (1024, 37), (4096, 300)])
+def test_adaln_modulate_wave_rows(dim, rows):
+    """The decoder's AdaLN tail (bf16, one vector pair for all rows): wave-per-row kernel, strided
+    over more rows than waves; one bf16 rounding of (x*r)*s1 + shift as the reference."""
+    x = torch.randn(rows, dim, device=DEV).to(BF)
+    sh = torch.randn(dim, device=DEV).to(BF)
+    s1 = (1 + 0.1 * torch.randn(dim, device=DEV)).to(BF)
+    y = torch.empty_like(x)
+    ops.adaln_modulate(x, sh, s1, 1e-5, y)
+    xf = x.float().cpu()
+    r = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)
+    close_bf16(y, rb(((xf * r) * s1.float().cpu()) + sh.float().cpu()))
+
+
 @pytest.mark.parametrize("dtype", [BF, torch.float32])
 def test_norms(dtype):
     x = torch.randn(37, 1280, device=DEV).to(dtype)
