@@ -1,0 +1,61 @@
+"""QKVG projection of the decoder, two ways, interleaved in one process (HIP events):
+  fused  — gemm_bf16_pp2_kernel<HEADNORM>: q/k RMSNorm + half RoPE in the GEMM epilogue
+  split  — persistent store GEMM (gemm_bf16_ps_kernel<STORE>) + head_norm_rope on the q/k blocks
+Both give bitwise-equal outputs (tests/test_gpu_kernels.py); this measures which is faster.
+    python tools/bench_qkvg.py [--rounds 5]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import echo_tts_amd  # noqa: E402
+from echo_tts_amd import ops  # noqa: E402
+from echo_tts_amd.model import MAX_POS, rope_table_cpu  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    dev, D, H, N = "cuda", 2048, 16, 640
+    torch.manual_seed(0)
+    w = (torch.randn(4 * D, D, device=dev) * 0.02).to(torch.bfloat16)
+    qk = (1 + 0.1 * torch.randn(2, H, 128, device=dev)).to(torch.bfloat16)
+    rope = rope_table_cpu(128, MAX_POS).to(dev)
+    for M in (30720, 10240):
+        x = torch.randn(M, D, device=dev).to(torch.bfloat16)
+        out = torch.empty(M, 4 * D, device=dev, dtype=torch.bfloat16)
+        hn = ops.HeadNorm(qk, H, 2, 1e-5, w_stride=H * 128, rope=rope, rope_heads=H // 2, seq_len=N, pos0=0)
+
+        def fused():
+            ops.gemm(x, w, out=out, head_norm=hn)
+
+        def split():
+            ops.gemm(x, w, out=out)
+            ops.head_norm_rope(out, H, qk, 1e-5, nblk=2, col0=0, col_stride=D, w_stride=H * 128, rope=rope,
+                               rope_heads=H // 2, seq_len=N, pos0=0, pos_mult=1)
+
+        fused()
+        a = out.clone()
+        split()
+        same = bool(torch.equal(a, out))
+        times = {"fused": [], "split": []}
+        for _ in range(args.rounds):
+            for name, fn in (("fused", fused), ("split", split)):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.iters):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                times[name].append(e0.elapsed_time(e1) / args.iters)
+        med = {k: sorted(v)[len(v) // 2] * 1e3 for k, v in times.items()}
+        print(f"M={M}: fused {med['fused']:.1f} us  split {med['split']:.1f} us  bitwise_equal={same}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
