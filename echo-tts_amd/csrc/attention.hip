@@ -67,8 +67,8 @@ __device__ __forceinline__ T sel4(int sg, T a0, T a1, T a2, T a3) {
 // 32-63 columns 8k+8 .. 8k+15, so gate loads and output stores are 16 B per lane (8 + 8 instead of
 // 16 + 16 8-B accesses; the store tail is issue-bound). Same roundings as the reference
 // (model.py:255-264: SDPA out bf16, sigmoid(gate) bf16, product bf16).
-__device__ __forceinline__ void attn_store_out(const f32x16 (&o)[4], float inv, int qi, int h2, bool valid,
-                                               bf16_t* op, const bf16_t* gp) {
+__device__ __forceinline__ void attn_pack_out(const f32x16 (&o)[4], float inv, int h2, bool valid, const bf16_t* gp,
+                                              uint4 (&v4)[8]) {
   uint32_t w[16][2];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -76,35 +76,45 @@ __device__ __forceinline__ void attn_store_out(const f32x16 (&o)[4], float inv, 
     w[k][0] = pack2bf(rbf(o[dt][4 * rg + 0] * inv), rbf(o[dt][4 * rg + 1] * inv));
     w[k][1] = pack2bf(rbf(o[dt][4 * rg + 2] * inv), rbf(o[dt][4 * rg + 3] * inv));
   }
-  uint4 v4[8];
 #pragma unroll
   for (int pk = 0; pk < 8; ++pk) {
     const auto x = __builtin_amdgcn_permlane32_swap(w[2 * pk][0], w[2 * pk + 1][0], false, false);
     const auto y = __builtin_amdgcn_permlane32_swap(w[2 * pk][1], w[2 * pk + 1][1], false, false);
     v4[pk] = make_uint4(x[0], y[0], x[1], y[1]);
   }
-  if (!valid) return;
+  if (!valid || !gp) return;
   const int c0 = 8 * h2;  // this lane's 8 columns of each 16-column pair
-  if (gp) {
-    uint4 g4[8];
+  uint4 g4[8];
 #pragma unroll
-    for (int pk = 0; pk < 8; ++pk) g4[pk] = *(const uint4*)(gp + 16 * pk + c0);
+  for (int pk = 0; pk < 8; ++pk) g4[pk] = *(const uint4*)(gp + 16 * pk + c0);
 #pragma unroll
-    for (int pk = 0; pk < 8; ++pk) {
-      const uint32_t vv[4] = {v4[pk].x, v4[pk].y, v4[pk].z, v4[pk].w};
-      const uint32_t gg[4] = {g4[pk].x, g4[pk].y, g4[pk].z, g4[pk].w};
-      uint32_t r[4];
+  for (int pk = 0; pk < 8; ++pk) {
+    const uint32_t vv[4] = {v4[pk].x, v4[pk].y, v4[pk].z, v4[pk].w};
+    const uint32_t gg[4] = {g4[pk].x, g4[pk].y, g4[pk].z, g4[pk].w};
+    uint32_t r[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float a0 = rbf(bf2f(vv[e] & 0xffffu) * rbf(sigmoid_f(bf2f(gg[e] & 0xffffu))));
-        const float a1 = rbf(bf2f(vv[e] >> 16) * rbf(sigmoid_f(bf2f(gg[e] >> 16))));
-        r[e] = pack2bf(a0, a1);
-      }
-      v4[pk] = make_uint4(r[0], r[1], r[2], r[3]);
+    for (int e = 0; e < 4; ++e) {
+      const float a0 = rbf(bf2f(vv[e] & 0xffffu) * rbf(sigmoid_f(bf2f(gg[e] & 0xffffu))));
+      const float a1 = rbf(bf2f(vv[e] >> 16) * rbf(sigmoid_f(bf2f(gg[e] >> 16))));
+      r[e] = pack2bf(a0, a1);
     }
+    v4[pk] = make_uint4(r[0], r[1], r[2], r[3]);
   }
+}
+
+// 8 16-B stores per valid lane (a wave with any valid lane issues exactly 8 store instructions)
+__device__ __forceinline__ void attn_write_out(const uint4 (&v4)[8], bf16_t* op, int h2, bool valid) {
+  if (!valid) return;
 #pragma unroll
-  for (int pk = 0; pk < 8; ++pk) *(uint4*)(op + 16 * pk + c0) = v4[pk];
+  for (int pk = 0; pk < 8; ++pk) *(uint4*)(op + 16 * pk + 8 * h2) = v4[pk];
+}
+
+__device__ __forceinline__ void attn_store_out(const f32x16 (&o)[4], float inv, int qi, int h2, bool valid,
+                                               bf16_t* op, const bf16_t* gp) {
+  (void)qi;
+  uint4 v4[8];
+  attn_pack_out(o, inv, h2, valid, gp, v4);
+  attn_write_out(v4, op, h2, valid);
 }
 
 // ---- shared by the bf16 kernels: per-workgroup segment table and tile cursors.
@@ -173,8 +183,15 @@ struct SegInfo {
 // filled by LDS-DMA (tile t+ST-1 issued at tile t); ST = 0 -> register staging (cdna_hip_programming.md
 // T14): tile t+2 is loaded into VGPRs at the top of tile t and written (swizzled) into the free LDS
 // buffer at the top of tile t+1, so 2 LDS buffers give a 2-tile lookahead.
-template <int ABL, int NW, int ST, int KTT = 64>
-__global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) attn_bf16_kernel(EchoAttnArgs a) {
+//
+// PS = 1: persistent form of the production schedule — gridDim.x workgroups walk the (q block, row,
+// head) items item = blockIdx.x + k * gridDim.x (same XCD for every k when gridDim.x % 8 == 0). An
+// item's gated output is stored after the NEXT item's Q loads and first K/V DMA have been issued, and
+// only those are waited for (vmcnt counts loads, LDS-DMA and stores in issue order), so the store
+// tail of one item overlaps the prologue of the next instead of a workgroup teardown + relaunch.
+template <int ABL, int NW, int ST, int KTT = 64, int PS = 0>
+__global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) attn_bf16_kernel(EchoAttnArgs a_arg) {
+  static_assert(!PS || (ABL == 0 && ST == 2), "persistent form: production schedule only");
   constexpr int QB = 32 * NW;
   constexpr int DPT = KTT / (4 * NW);  // DMA wave-instructions per wave per K (or V) tile
   const uint64_t ts0 = (ABL & 128) ? rt_now() : 0;
@@ -183,17 +200,32 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
   constexpr int NBUF = ST == 0 ? 2 : ST;
   __shared__ __attribute__((aligned(16))) bf16_t lds[NBUF * 2 * KTT * 128];
 
-  const int nqb = (a.n_q + QB - 1) / QB;
-  const int L = remap_xcd(blockIdx.x, gridDim.x);
+  // the arguments are read through the kernarg segment pointer; in the persistent form it is
+  // laundered per item, so hipcc re-reads them instead of hoisting the ~50 scalars of the segment
+  // table out of the item loop (where they spill)
+  using KArgs = const __attribute__((address_space(4))) EchoAttnArgs;
+  KArgs* const kargs = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  (void)a_arg;
+  const int nqb = (kargs->n_q + QB - 1) / QB;
+  const int nitems = PS ? nqb * kargs->rows * kargs->heads : (int)blockIdx.x + 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h2 = lane >> 5, ql = lane & 31;
+  uint4 pend[8];  // PS: the previous item's gated output, not yet stored
+  bf16_t* pend_op = nullptr;
+  bool pend_valid = false, pend_any = false;
+  int item = blockIdx.x;
+  do {
+  KArgs* kap = kargs;
+  if constexpr (PS) asm volatile("" : "+s"(kap));
+  KArgs& a = *kap;
+  const int L = remap_xcd(item, PS ? nitems : (int)gridDim.x);
   const int qb = L % nqb;
   // rows fastest: each XCD's contiguous block range then covers every row type (cond /
   // uncond-text / uncond-speaker rows have different key counts), and the CFG rows that share
   // one text/speaker K/V copy land on the same XCD
   const int row = (L / nqb) % a.rows;
   const int head = L / (nqb * a.rows);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h2 = lane >> 5, ql = lane & 31;
   const int q0 = qb * QB;
   const int qi = q0 + w * 32 + ql;
   const int qc = min(qi, a.n_q - 1);
@@ -203,9 +235,11 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
 #pragma unroll
   for (int ds = 0; ds < 8; ++ds) qf[ds] = *(const bf16x8*)(qp + 16 * ds + 8 * h2);
   // consume Q here so hipcc waits for it once, not inside the tile loop (where its counted
-  // waits would land on the asm DMA of the next tile)
+  // waits would land on the asm DMA of the next tile); PS: after the pending stores are issued
+  if constexpr (!PS) {
 #pragma unroll
-  for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));
+    for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));
+  }
 
   // flat list of 64-key tiles over the (up to 4) segments; per-segment fields are kept in
   // named scalars (no runtime-indexed arrays: those go to scratch)
@@ -276,10 +310,25 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
 #pragma unroll
     for (int p = 0; p < ST - 1; ++p)
       if (p < ntiles) dma_tile(p);
-    if (ST == 3 && ntiles > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPT) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (ST == 3 && ntiles > 1) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPT) : "memory");
+    } else if (PS && pend_any) {
+      // the previous item's 8 stores go behind Q + tile 0 and stay in flight
+      asm volatile("" ::: "memory");
+      attn_write_out(pend, pend_op, h2, pend_valid);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
-  __syncthreads();
+  if constexpr (PS) {
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // raw: __syncthreads' release fence would wait for the stores
+  } else {
+    __syncthreads();
+  }
 
   const uint64_t ts1 = (ABL & 128) ? rt_now() : 0;
   int cur = 0;
@@ -471,11 +520,24 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) at
     bf16_t* op = (bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qc * a.o_ld_tok + head * 128;
     const bf16_t* gp = a.gate ? (const bf16_t*)a.gate + row * a.g_ld_batch + (int64_t)qc * a.g_ld_tok + head * 128
                               : nullptr;
-    attn_store_out(o, inv, qi, h2, valid, op, gp);
+    if constexpr (PS) {
+      attn_pack_out(o, inv, h2, valid, gp, pend);
+      pend_op = op;
+      pend_valid = valid;
+      pend_any = __any(valid);
+    } else {
+      attn_store_out(o, inv, qi, h2, valid, op, gp);
+    }
   }
   if ((ABL & 128) && threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     g_attn_stamps[(int64_t)blockIdx.x * 6 + 3] = rt_now();
+  }
+  if constexpr (!PS) break;
+  item += gridDim.x;
+  } while (item < nitems);  // item loop
+  if constexpr (PS) {
+    if (pend_any) attn_write_out(pend, pend_op, h2, pend_valid);
   }
 }
 
@@ -813,10 +875,22 @@ int check_attn_args(const EchoAttnArgs* a) {
 
 int attn_grid(const EchoAttnArgs* a, int qb) { return ((a->n_q + qb - 1) / qb) * a->heads * a->rows; }
 
+// persistent grid: two workgroups per CU (a multiple of 8, so an item's XCD is its block's XCD)
+int attn_ps_grid(int nitems) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      return -1;
+    cus = n;
+  }
+  return min(nitems, (2 * cus + 7) / 8 * 8);
+}
+
 // Measurement variants of the bf16 kernel (tools/bench_attn.py; DESIGN.md §7 lists what each
 // showed). variant: 0 production (4 waves, 2-slot LDS-DMA ring, 64-key tiles), 1/2 8 waves with
 // a 2/3-slot ring, 3/4 register-staged K/V with 4/8 waves, 5 software-pipelined kernel (two waves
-// per SIMD), 6/7 32-key tiles with a 2/3-slot ring. ablation: the ABL bits of attn_bf16_kernel.
+// per SIMD), 6/7 32-key tiles with a 2/3-slot ring, 8 the persistent form of 0. ablation: the ABL bits of attn_bf16_kernel.
 int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) {
   const int qb = (cfg == 1 || cfg == 2 || cfg == 4) ? 256 : 128;
   const dim3 grid(attn_grid(a, qb));
@@ -853,6 +927,13 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       else if (abl == 0) hipLaunchKernelGGL((attn_pipe_kernel<0>), grid, dim3(256), 0, s, *a);
       else return ECHO_EINVAL;
       break;
+    case 8: {  // persistent form: two workgroups per CU
+      if (abl) return ECHO_EINVAL;
+      const int ps_grid = attn_ps_grid(grid.x);
+      if (ps_grid <= 0) return ECHO_EINVAL;
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a);
+      break;
+    }
     case 6: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 2, 32); break;
     case 7: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 3, 32); break;
     default: return ECHO_EINVAL;
@@ -870,7 +951,17 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   if (a->dtype == ECHO_BF16) {
-    hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a);
+    // the persistent form (variant 8, bitwise equal) for 1-3 items per workgroup slot: there its
+    // store/prologue overlap wins (sampler R = 16: 152.7 -> 146.9 us); at more items the static
+    // item order cannot balance rows of unequal key counts the way the dispatcher does (R = 48: equal
+    // or slower), and at <= 1 item it is the same kernel
+    const int nitems = attn_grid(a, 128);
+    const int ps_grid = attn_ps_grid(nitems);
+    if (ps_grid <= 0) return ECHO_EINVAL;
+    if (nitems > ps_grid && nitems <= 3 * ps_grid)
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a);
+    else
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(nitems), dim3(256), 0, s, *a);
   } else {
     hipLaunchKernelGGL(attn_f32_kernel, dim3(attn_grid(a, FQ)), dim3(64), 0, s, *a);
   }

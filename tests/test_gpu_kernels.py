@@ -271,7 +271,7 @@ def ref_attention(q, segs, gate, scale, dtype):
     return o
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 def test_attention_variants_match_production(variant):
     """Diagnostic entry point: every measurement variant computes the production result
     (variant 0 bitwise; the others up to accumulation-order rounding), and the timeline
@@ -286,7 +286,7 @@ def test_attention_variants_match_production(variant):
     ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
     got = torch.empty_like(ref)
     ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=variant)
-    if variant == 0:
+    if variant in (0, 8):
         assert torch.equal(got, ref)
     else:
         close_bf16(got, ref.float().cpu())
@@ -297,6 +297,40 @@ def test_attention_variants_match_production(variant):
         torch.cuda.synchronize()
         n = ((N + 32 * (4 if variant in (0, 3) else 8) - 1) // (32 * (4 if variant in (0, 3) else 8))) * H * R
         assert (st[:n, 3] >= st[:n, 0]).all() and (st[:n, 0] > 0).all()
+
+
+@pytest.mark.parametrize("n_q,cfg", [(640, True), (600, True), (640, False), (600, False)])
+def test_attention_persistent_multi_item(n_q, cfg):
+    """The persistent attention kernel (variant 8; production for 1-3 items per workgroup slot, e.g.
+    the sampler's R = 16 phase): with more (q block, row, head) items than its 2-per-CU grid, each
+    workgroup runs several items and stores an item's output behind the next item's loads. Bitwise
+    equal to the one-item-per-workgroup kernel (variant 0) at the sampler's shapes (R = 48 / 16),
+    with ragged text lengths (incl. 0) and, for n_q = 600, a last q block whose fourth wave has no
+    valid query (no pending stores for that wave)."""
+    B, H, T, P = 16, 16, 448, 160
+    R = 3 * B if cfg else B
+    qkvg = torch.randn(R, n_q, 4, H, 128, device=DEV).to(BF)
+    kt = torch.randn(B, T, 2, H, 128, device=DEV).to(BF)
+    ks = torch.randn(B, P, 2, H, 128, device=DEV).to(BF)
+    g = torch.Generator().manual_seed(3)
+    tl_b = torch.randint(0, T + 1, (B,), generator=g).tolist()
+    tl = torch.tensor((tl_b + [0] * B + tl_b)[:R], dtype=torch.int32, device=DEV)
+    sl = torch.tensor(([P] * 2 * B + [0] * B)[:R], dtype=torch.int32, device=DEV)
+    segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2]),
+            ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=B),
+            ops.Segment(ks[:, :, 0], ks[:, :, 1], lens=sl, batch_mod=B)]
+    got = torch.full((R, n_q, H, 128), float("nan"), device=DEV, dtype=BF)
+    ref = torch.empty_like(got)
+    ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=8)
+    ops.attention_variant(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3], variant=0)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    # production (persistent or not by item count) and a repeat on the same buffers
+    got.fill_(float("nan"))
+    ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
+    assert torch.equal(got, ref)
+    ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=8)
+    assert torch.equal(got, ref)
 
 
 def test_attention_engine_kv_layout():

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--variant", type=int, default=None, help="echo_attention_variant variant id (diagnostics)")
     ap.add_argument("--ablation", type=int, default=0, help="ablation bits (timing only, results wrong)")
     ap.add_argument("--stamps", default=None, help="ablation 128: write the last call's timeline (.npy)")
+    ap.add_argument("--compare", default=None, help="two variant ids 'A,B': interleaved rounds + bitwise check")
     args = ap.parse_args()
     dev = "cuda"
     B, N, H, T, P = 16, 640, 16, 448, 160
@@ -51,6 +52,22 @@ def main():
             segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2], batch_mod=bm_self),
                     ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=bm_c),
                     ops.Segment(ks[:, :, 0], ks[:, :, 1], lens=sl, batch_mod=bm_c)]
+            if args.compare:
+                va, vb = (int(v) for v in args.compare.split(","))
+                fa = lambda v: ops.attention_variant(qkvg[:, :, 0], segs, out=out, gate=qkvg[:, :, 3],  # noqa: E731
+                                                     variant=v, ablation=0, stamps=None)
+                fa(va)
+                ref = out.clone()
+                fa(vb)
+                same = bool(torch.equal(ref, out))
+                ta, tb = [], []
+                for _ in range(5):
+                    ta.append(timeit(lambda: fa(va), rounds=1))
+                    tb.append(timeit(lambda: fa(vb), rounds=1))
+                ma, mb = sorted(ta)[2], sorted(tb)[2]
+                print(f"R={R:3d} {name:10s} v{va} {ma * 1e3:8.1f} us  v{vb} {mb * 1e3:8.1f} us  "
+                      f"bitwise_equal={same}", flush=True)
+                continue
             if args.variant is None and not args.ablation:
                 fn = lambda: ops.attention(qkvg[:, :, 0], segs, out=out, gate=qkvg[:, :, 3])  # noqa: E731
             else:
