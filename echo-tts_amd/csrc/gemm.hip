@@ -70,8 +70,9 @@ __device__ __forceinline__ float epi_pointwise(float v, const Epi& ep, int n) {
 
 // Epilogue kinds, resolved on the host (ek_of) so the hot GEMMs get straight-line code:
 // EK_GENERIC handles every Epi combination with runtime flags; the specialised kinds cover the
-// decoder's three hot shapes (QKVG store, W13 SwiGLU, Wo/W2 gated residual) without bias/act/div.
-enum { EK_GENERIC = 0, EK_STORE = 1, EK_SWIGLU = 2, EK_RESID = 3, EK_HEADNORM = 4 };
+// decoder's three hot shapes (QKVG store, W13 SwiGLU, Wo/W2 gated residual) without bias/act/div;
+// EK_BIAS (store + bias, the decoder's input projection) exists in the persistent kernel only.
+enum { EK_GENERIC = 0, EK_STORE = 1, EK_SWIGLU = 2, EK_RESID = 3, EK_HEADNORM = 4, EK_BIAS = 5 };
 
 // SiLU for the SwiGLU epilogue: hardware exp2 + reciprocal (≈2 ulp fp32 before the bf16 rounding
 // that follows; the reference's bf16 F.silu rounds the same value, model.py:118-122).
@@ -710,7 +711,7 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
                     const bf16_t* __restrict__ W, int64_t ldw, int64_t sW,
                     void* __restrict__ Cv, int64_t ldc, int64_t sC,
                     int M, int N, int K, int tiles_m, int tiles_n, Epi ep) {
-  static_assert(EK == EK_STORE || EK == EK_SWIGLU || EK == EK_RESID, "register epilogue kinds");
+  static_assert(EK == EK_STORE || EK == EK_SWIGLU || EK == EK_RESID || EK == EK_BIAS, "register epilogue kinds");
   constexpr int BM = 256, BN = 256, TM = 128, TN = 64, FM = 8, FN = 4;
   constexpr int STAGE = (BM + BN) * BK;
   constexpr int SN = reg_epi_stores(EK);
@@ -775,12 +776,22 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   int m0, n0;
   origin(t, m0, n0);
   setup(m0, n0);
+  // EK_BIAS: the bias of this lane's accumulator columns (n0 + wn*TN + j*16 + cq + r) of a tile is
+  // loaded just before the tile's prologue DMA (older than every DMA the K loop waits for, so the
+  // counted waits are unchanged) and consumed after the K loop's final vmcnt(0)
+  const int cq = 4 * (lane >> 4);
+  uint2 bb[FN], bbn[FN];
+  auto load_bias = [&](int n0t, uint2 (&d)[FN]) __attribute__((always_inline)) {
+    const bf16_t* bp = (const bf16_t*)ep.bias + z * ep.stride_bias + n0t + wn * TN + cq;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) d[j] = *(const uint2*)(bp + j * 16);
+  };
+  if constexpr (EK == EK_BIAS) load_bias(n0, bb);
   prologue();
 
   const __amdgpu_buffer_rsrc_t crs = brsrc((bf16_t*)Cv + z * sC, (uint32_t)(((int64_t)(M - 1) * ldc + N) * 2));
   const int frow = lane & 15;
   const int fsw = frow >> 1;
-  const int cq = 4 * (lane >> 4);
   bool first = true;
   for (;;) {
     if (first) vm_wait_n<8>(); else vm_wait_n<8 + SN>();
@@ -840,6 +851,10 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
     if (wm == 0) pp_barrier();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // every wave's last fragment reads are done: both LDS buffers are free
+    if constexpr (EK == EK_BIAS) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(bb[j].x), "v"(bb[j].y));
+    }
 
     const int tnext = t + gridDim.x;
     const bool more = tnext < ntl;
@@ -879,6 +894,7 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
     if (more) {
       origin(tnext, m0n, n0n);
       setup(m0n, n0n);
+      if constexpr (EK == EK_BIAS) load_bias(n0n, bbn);
       prologue();
     }
     if constexpr (EK == EK_RESID) {
@@ -912,8 +928,16 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
         const uint32_t off = (uint32_t)(((mb + ii * 16) * ldc + nb) * 2);
 #pragma unroll
         for (int p = 0; p < FN / 2; ++p) {
-          const f32x4& c0 = acc[ii][2 * p];
-          const f32x4& c1 = acc[ii][2 * p + 1];
+          f32x4 c0 = acc[ii][2 * p];
+          f32x4 c1 = acc[ii][2 * p + 1];
+          if constexpr (EK == EK_BIAS) {
+            // acc + bias in fp32, rounded once (gemm_epilogue's generic kind: x += bias; rbf)
+            const uint2 b0 = bb[2 * p], b1 = bb[2 * p + 1];
+            c0[0] += bf2f(b0.x & 0xffffu); c0[1] += bf2f(b0.x >> 16);
+            c0[2] += bf2f(b0.y & 0xffffu); c0[3] += bf2f(b0.y >> 16);
+            c1[0] += bf2f(b1.x & 0xffffu); c1[1] += bf2f(b1.x >> 16);
+            c1[2] += bf2f(b1.y & 0xffffu); c1[3] += bf2f(b1.y >> 16);
+          }
           u32x4 o = swap_pair(make_uint2(pack2bf(c0[0], c0[1]), pack2bf(c0[2], c0[3])),
                               make_uint2(pack2bf(c1[0], c1[1]), pack2bf(c1[2], c1[3])));
           if constexpr (EK == EK_RESID) {
@@ -935,6 +959,10 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
     t = tnext;
     m0 = m0n;
     n0 = n0n;
+    if constexpr (EK == EK_BIAS) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bb[j] = bbn[j];
+    }
     first = false;
   }
 }
@@ -1226,6 +1254,9 @@ int launch_ps_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 
 // epilogue kind of a call: the specialised kinds need no bias, no activation and no divisor
 int ek_of(const EchoGemmArgs* a) {
+  if (a->bias && a->act == ECHO_ACT_NONE && a->out_div == 0.0f && a->epilogue == ECHO_EPI_STORE &&
+      a->dtype == ECHO_BF16)
+    return EK_BIAS;  // persistent kernel only; the other launchers take it as EK_GENERIC
   if (a->bias || a->act != ECHO_ACT_NONE || a->out_div != 0.0f) return EK_GENERIC;
   switch (a->epilogue) {
     case ECHO_EPI_STORE: return EK_STORE;
@@ -1248,7 +1279,7 @@ int launch_bf16(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 
 // persistent kernel: register epilogues only, K >= 128, and 32-bit buffer offsets for C / aux
 bool ps_ok(const EchoGemmArgs* a, int ek) {
-  if (ek != EK_STORE && ek != EK_SWIGLU && ek != EK_RESID) return false;
+  if (ek != EK_STORE && ek != EK_SWIGLU && ek != EK_RESID && ek != EK_BIAS) return false;
   if (a->K < 128 || a->N % 256) return false;
   const int64_t lim = (int64_t)1 << 30;  // elements: 32-bit byte offsets (rows up to M + 255)
   if ((int64_t)(a->M + 255) * a->ldc >= lim || (int64_t)a->M * a->lda >= lim || (int64_t)a->N * a->ldw >= lim)
@@ -1263,6 +1294,7 @@ int launch_ps(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
     case EK_STORE: return launch_ps_ek<EK_STORE, CP>(a, ep, s);
     case EK_SWIGLU: return launch_ps_ek<EK_SWIGLU, CP>(a, ep, s);
     case EK_RESID: return launch_ps_ek<EK_RESID, CP>(a, ep, s);
+    case EK_BIAS: return launch_ps_ek<EK_BIAS, CP>(a, ep, s);
     default: return ECHO_EINVAL;
   }
 }

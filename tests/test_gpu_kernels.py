@@ -155,6 +155,28 @@ def test_gemm_persistent_bitwise(M, N, K, epi):
         assert torch.equal(b0, b1)
 
 
+@pytest.mark.parametrize("M,N,K", [(4133, 4096, 192), (300, 512, 128), (30720, 2048, 128), (10240, 2048, 128)])
+def test_gemm_persistent_bias_bitwise(M, N, K):
+    """Store + bias (the decoder's input projection, K = 128) runs the persistent kernel's EK_BIAS
+    register epilogue (auto tile, incl. the row split at M = 10240) and equals the generic
+    LDS-staged epilogue of the 2-phase kernel and of the small-tile kernel bitwise (acc + bias in
+    fp32, one rounding); output a column slice of a wider buffer."""
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    b = torch.randn(N, device=DEV).to(BF)
+    h = torch.randn(M, N + 256, device=DEV).to(BF)
+    outs = []
+    for tile in (13, 16, 0, 5):
+        buf = h.clone()
+        ops.gemm(a, w, out=buf[:, :N], bias=b, tile=tile)
+        assert torch.equal(buf[:, N:], h[:, N:])
+        outs.append(buf)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    ref = (a.float() @ w.float().t() + b.float()).to(BF)
+    close_bf16(outs[0][:, :N], ref.cpu().float())
+
+
 @pytest.mark.parametrize("epi", [L.EPI_STORE, L.EPI_RESID, L.EPI_F32OUT])
 def test_gemm_row_split_bitwise(epi):
     """Auto-tiled 10240x2048 launches split rows into whole 256x256 rounds + a smaller-tile tail;

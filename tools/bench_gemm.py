@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--torch", action="store_true", help="also time torch.nn.functional.linear (hipBLASLt)")
     ap.add_argument("--shapes", default=None, help="M,N,K[,epi];... overrides the production list")
+    ap.add_argument("--bias", action="store_true", help="add a bias vector (generic epilogue kind)")
     ap.add_argument("--stagger", type=int, default=0, help="tile 14: first-round group delay (10 ns ticks)")
     args = ap.parse_args()
     if args.stagger:
@@ -67,10 +68,11 @@ def main():
         nout = N // 2 if epi == L.EPI_SWIGLU else N
         aux = torch.randn(M, nout, device=dev).to(torch.bfloat16)
         gate = torch.randn(nout, device=dev).to(torch.bfloat16) if epi == L.EPI_RESID else None
+        bias = torch.randn(nout, device=dev).to(torch.bfloat16) if args.bias else None
         outs = {}
         for t in tiles:
             o = aux.clone() if epi == L.EPI_RESID else torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
-            ops.gemm(a, w, out=o, epilogue=epi, aux=o if epi == L.EPI_RESID else None, gate=gate, tile=t)
+            ops.gemm(a, w, out=o, epilogue=epi, aux=o if epi == L.EPI_RESID else None, gate=gate, bias=bias, tile=t)
             outs[t] = o
         base = outs[tiles[0]]
         same = {t: bool(torch.equal(outs[t], base)) for t in tiles}
@@ -82,7 +84,7 @@ def main():
                 e0.record()
                 for _ in range(args.iters):
                     ops.gemm(a, w, out=out, epilogue=epi, aux=aux if epi == L.EPI_RESID else None, gate=gate,
-                             tile=t)
+                             bias=bias, tile=t)
                 e1.record()
                 torch.cuda.synchronize()
                 times[t].append(e0.elapsed_time(e1) / args.iters)
