@@ -32,7 +32,8 @@ struct Epi {
   // ECHO_EPI_HEADNORM
   const void* hn_w; int64_t hn_w_stride; const float* hn_rope;
   int hn_heads, hn_nblk, hn_rope_heads, hn_seq_len, hn_pos0, hn_pos_mult; float hn_eps;
-  int stagger;  // diagnostic (tile 14): first-round start delay per CU group, 10 ns ticks
+  int stagger;  // pp2 diagnostic (tile 14): first-round start delay per CU group, 10 ns ticks;
+                // persistent kernel: group-M height (set by launch_ps_ek)
   const void* act_alpha;        // ECHO_ACT_SNAKE
   int conv_c, conv_taps, conv_dil;  // causal-conv A addressing (echo_hip.h)
 };
@@ -725,7 +726,9 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   W += z * sW;
   const int ntl = tiles_m * tiles_n;
   const int q8 = ntl >> 3, r8 = ntl & 7;
-  constexpr int GM = 8;
+  // group-M height, chosen on the host (launch_ps_ek; tile 18: diagnostic override) and passed in
+  // ep.stagger, which this kernel does not otherwise use
+  const int GM = ep.stagger > 0 ? ep.stagger : 8;
   // tile t -> origin: gemm_bf16_pp2_kernel's XCD-chunked group-M order with t in place of the
   // block id (t = blockIdx.x + r * gridDim.x keeps t & 7 = the XCD when gridDim.x % 8 == 0)
   auto origin = [&](int t, int& m0, int& n0) __attribute__((always_inline)) {
@@ -1245,9 +1248,14 @@ int launch_ps_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
     g_num_cus = n;
   }
   const int grid = min(tm * tn, g_num_cus);
+  // group-M height 8. Measured with tile 18 (tools/bench_gemm.py --stagger G): 1, 2, 4 and 16 are
+  // 2-6 % slower on QKVG/W13; on the N = 2048 residual GEMMs 4 was within +-2 % of 8 in either
+  // direction across two boxes (Wo 245 vs 252 / 235 vs 229 us, W2 591 vs 604 / 579 vs 587 us)
+  Epi e = ep;
+  if (e.stagger <= 0) e.stagger = 8;
   hipLaunchKernelGGL((gemm_bf16_ps_kernel<EK, CP>), dim3(grid, a->batch), dim3(512), 0, s, (const bf16_t*)a->A,
                      a->lda, a->stride_a, (const bf16_t*)a->W, a->ldw, a->stride_w, a->C, a->ldc, a->stride_c,
-                     a->M, a->N, a->K, tm, tn, ep);
+                     a->M, a->N, a->K, tm, tn, e);
   ECHO_LAUNCH_CHECK();
   return 0;
 }
@@ -1357,7 +1365,7 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
          a->epilogue, a->act, a->out_div,
          a->hn_w, a->hn_w_stride, a->hn_rope, a->hn_heads, a->hn_nblk, a->hn_rope_heads, a->hn_seq_len,
          a->hn_pos0, a->hn_pos_mult, a->hn_eps, 0, a->act_alpha, a->conv_c, a->conv_taps, a->conv_dil};
-  if (a->tile == 14) ep.stagger = g_gemm_stagger;
+  if (a->tile == 14 || a->tile == 18) ep.stagger = g_gemm_stagger;
   if (a->tile == 15) ep.epi = 99;  // diagnostic: no epilogue
   int t = a->tile > 0 ? a->tile : pick_tile(a->M, a->N, a->K, a->batch);
   // 256x256 tiles run the persistent 2-phase kernel where its register epilogue applies, else the
@@ -1424,6 +1432,7 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
     case 13: case 14: case 15: return launch_pp2(a, ep, s);
     case 16: return ps_ok(a, ek_of(a)) ? launch_ps(a, ep, s) : launch_pp2(a, ep, s);
     case 17: return ps_ok(a, ek_of(a)) ? launch_ps<2>(a, ep, s) : launch_pp2(a, ep, s);
+    case 18: return ps_ok(a, ek_of(a)) ? launch_ps(a, ep, s) : ECHO_EINVAL;  // group-M override (diag key 1)
     default: return ECHO_EINVAL;
   }
 }

@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--torch", action="store_true", help="also time torch.nn.functional.linear (hipBLASLt)")
     ap.add_argument("--shapes", default=None, help="M,N,K[,epi];... overrides the production list")
+    ap.add_argument("--pad-a", type=int, default=0, help="row stride of A = K + pad (elements)")
+    ap.add_argument("--pad-c", type=int, default=0, help="row stride of the output = N + pad (elements)")
     ap.add_argument("--bias", action="store_true", help="add a bias vector (generic epilogue kind)")
     ap.add_argument("--stagger", type=int, default=0, help="tile 14: first-round group delay (10 ns ticks)")
     args = ap.parse_args()
@@ -63,7 +65,7 @@ def main():
     dev = "cuda"
     torch.manual_seed(0)
     for name, M, N, K, epi in shapes:
-        a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        a = torch.randn(M, K + args.pad_a, device=dev).to(torch.bfloat16)[:, :K]
         w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
         nout = N // 2 if epi == L.EPI_SWIGLU else N
         aux = torch.randn(M, nout, device=dev).to(torch.bfloat16)
@@ -77,7 +79,7 @@ def main():
         base = outs[tiles[0]]
         same = {t: bool(torch.equal(outs[t], base)) for t in tiles}
         times = {t: [] for t in tiles}
-        out = torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
+        out = torch.empty(M, nout + args.pad_c, device=dev, dtype=torch.bfloat16)[:, :nout]
         for _ in range(args.rounds):
             for t in tiles:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
