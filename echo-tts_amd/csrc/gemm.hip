@@ -1180,6 +1180,15 @@ int pick_tile(int M, int N, int K, int batch) {
     const double est = tile_cost(c, M, N, batch);
     if (est < best_t * 0.999) { best_t = est; best = c + 1; }
   }
+  // Under-filled launches (fewer tiles than CUs) are latency-bound per workgroup, which the
+  // throughput model does not see: take the largest multi-block config that still gives every CU
+  // a tile, else the one with the most tiles (tools/bench_gemm.py, e.g. M=1920 N=2048 K=5888:
+  // 256x128 86.7 us, 128x64 61.6 us; M=640 N=80: 39.7 -> 14.2 us on 64x64)
+  auto ntiles = [&](int c) { return (double)((M + kTiles[c].bm - 1) / kTiles[c].bm) * ((N + kTiles[c].bn - 1) / kTiles[c].bn) * batch; };
+  if (ntiles(best - 1) < 256) {
+    for (int c = 2; c < 5; ++c)
+      if (ntiles(c) >= 256 || c == 4) return c + 1;
+  }
   return best;
 }
 

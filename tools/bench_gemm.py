@@ -73,13 +73,15 @@ def main():
         bias = torch.randn(nout, device=dev).to(torch.bfloat16) if args.bias else None
         outs = {}
         for t in tiles:
-            o = aux.clone() if epi == L.EPI_RESID else torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
+            odt = torch.float32 if epi == L.EPI_F32OUT else torch.bfloat16
+            o = aux.clone() if epi == L.EPI_RESID else torch.empty(M, nout, device=dev, dtype=odt)
             ops.gemm(a, w, out=o, epilogue=epi, aux=o if epi == L.EPI_RESID else None, gate=gate, bias=bias, tile=t)
             outs[t] = o
         base = outs[tiles[0]]
         same = {t: bool(torch.equal(outs[t], base)) for t in tiles}
         times = {t: [] for t in tiles}
-        out = torch.empty(M, nout + args.pad_c, device=dev, dtype=torch.bfloat16)[:, :nout]
+        out = torch.empty(M, nout + args.pad_c, device=dev,
+                          dtype=torch.float32 if epi == L.EPI_F32OUT else torch.bfloat16)[:, :nout]
         for _ in range(args.rounds):
             for t in tiles:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
