@@ -190,7 +190,7 @@ struct SegInfo {
 // only those are waited for (vmcnt counts loads, LDS-DMA and stores in issue order), so the store
 // tail of one item overlaps the prologue of the next instead of a workgroup teardown + relaunch.
 template <int ABL, int NW, int ST, int KTT = 64, int PS = 0>
-__global__ void __launch_bounds__(64 * NW, NW == 4 ? (KTT == 32 ? 3 : 2) : 1) attn_bf16_kernel(EchoAttnArgs a_arg) {
+__global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1) attn_bf16_kernel(EchoAttnArgs a_arg) {
   static_assert(!PS || (ABL == 0 && ST == 2), "persistent form: production schedule only");
   constexpr int QB = 32 * NW;
   constexpr int DPT = KTT / (4 * NW);  // DMA wave-instructions per wave per K (or V) tile
@@ -890,7 +890,8 @@ int attn_ps_grid(int nitems) {
 // Measurement variants of the bf16 kernel (tools/bench_attn.py; DESIGN.md §7 lists what each
 // showed). variant: 0 production (4 waves, 2-slot LDS-DMA ring, 64-key tiles), 1/2 8 waves with
 // a 2/3-slot ring, 3/4 register-staged K/V with 4/8 waves, 5 software-pipelined kernel (two waves
-// per SIMD), 6/7 32-key tiles with a 2/3-slot ring, 8 the persistent form of 0. ablation: the ABL bits of attn_bf16_kernel.
+// per SIMD), 6/7 32-key tiles with a 2/3-slot ring, 8 the persistent form of 0, 9 two waves
+// (64 queries) per workgroup. ablation: the ABL bits of attn_bf16_kernel.
 int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) {
   const int qb = (cfg == 1 || cfg == 2 || cfg == 4) ? 256 : 128;
   const dim3 grid(attn_grid(a, qb));
@@ -935,6 +936,10 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       break;
     }
     case 6: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 2, 32); break;
+    case 9:  // 2 waves x 32 queries per workgroup (production for launches that cannot fill the CUs)
+      if (abl) return ECHO_EINVAL;
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 2, 2>), dim3(attn_grid(a, 64)), dim3(128), 0, s, *a);
+      break;
     case 7: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 3, 32); break;
     default: return ECHO_EINVAL;
   }
@@ -958,6 +963,9 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
     const int nitems = attn_grid(a, 128);
     const int ps_grid = attn_ps_grid(nitems);
     if (ps_grid <= 0) return ECHO_EINVAL;
+    // (fewer items than CUs, B = 1: 64-query workgroups — variant 9, bitwise equal — are slower,
+    // R = 3: 43.2 -> 54.1 us, R = 1: 38.7 -> 47.1 us: the per-workgroup tile chain stays as long and
+    // each wave issues twice the DMA; that case needs split-KV chains)
     if (nitems > ps_grid && nitems <= 3 * ps_grid)
       hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a);
     else

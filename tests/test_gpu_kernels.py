@@ -293,7 +293,7 @@ def ref_attention(q, segs, gate, scale, dtype):
     return o
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_attention_variants_match_production(variant):
     """Diagnostic entry point: every measurement variant computes the production result
     (variant 0 bitwise; the others up to accumulation-order rounding), and the timeline
@@ -308,7 +308,7 @@ def test_attention_variants_match_production(variant):
     ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
     got = torch.empty_like(ref)
     ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=variant)
-    if variant in (0, 8):
+    if variant in (0, 8, 9):
         assert torch.equal(got, ref)
     else:
         close_bf16(got, ref.float().cpu())
@@ -319,6 +319,32 @@ def test_attention_variants_match_production(variant):
         torch.cuda.synchronize()
         n = ((N + 32 * (4 if variant in (0, 3) else 8) - 1) // (32 * (4 if variant in (0, 3) else 8))) * H * R
         assert (st[:n, 3] >= st[:n, 0]).all() and (st[:n, 0] > 0).all()
+
+
+@pytest.mark.parametrize("B", [1, 3])
+@pytest.mark.parametrize("n_q", [640, 600, 200])
+def test_attention_small_batch_two_wave(B, n_q):
+    """B = 1 sampling (3 CFG rows, then 1 row) cannot fill the CUs with 128-query workgroups: the
+    production path and the 64-query-workgroup variant 9 are bitwise equal to variant 0 there."""
+    H, T, P = 16, 448, 160
+    for R in (3 * B, B):
+        qkvg = torch.randn(R, n_q, 4, H, 128, device=DEV).to(BF)
+        kt = torch.randn(B, T, 2, H, 128, device=DEV).to(BF)
+        ks = torch.randn(B, P, 2, H, 128, device=DEV).to(BF)
+        tl = torch.tensor(([300] * B + [0] * B + [300] * B)[:R], dtype=torch.int32, device=DEV)
+        sl = torch.tensor(([P] * 2 * B + [0] * B)[:R], dtype=torch.int32, device=DEV)
+        segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2]),
+                ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=B),
+                ops.Segment(ks[:, :, 0], ks[:, :, 1], lens=sl, batch_mod=B)]
+        got = torch.full((R, n_q, H, 128), float("nan"), device=DEV, dtype=BF)
+        ref = torch.empty_like(got)
+        ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
+        ops.attention_variant(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3], variant=0)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref)
+        got.fill_(float("nan"))
+        ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=9)
+        assert torch.equal(got, ref)
 
 
 @pytest.mark.parametrize("n_q,cfg", [(640, True), (600, True), (640, False), (600, False)])

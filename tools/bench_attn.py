@@ -32,10 +32,11 @@ def main():
     ap.add_argument("--variant", type=int, default=None, help="echo_attention_variant variant id (diagnostics)")
     ap.add_argument("--ablation", type=int, default=0, help="ablation bits (timing only, results wrong)")
     ap.add_argument("--stamps", default=None, help="ablation 128: write the last call's timeline (.npy)")
+    ap.add_argument("--batch", type=int, default=16, help="prompts B (rows 3B with CFG, B without)")
     ap.add_argument("--compare", default=None, help="two variant ids 'A,B': interleaved rounds + bitwise check")
     args = ap.parse_args()
     dev = "cuda"
-    B, N, H, T, P = 16, 640, 16, 448, 160
+    B, N, H, T, P = args.batch, 640, 16, 448, 160
     for R, tl_c, sl_c in ((3 * B, [388] * B + [0] * B + [388] * B, [160] * 2 * B + [0] * B),
                           (B, [388] * B, [160] * B)):
         if args.rows and R != args.rows:
