@@ -87,7 +87,9 @@ int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch);
 
 /* Diagnostic knobs for tools/bench_gemm.py (not used by the product path). key 1: start delay
  * between the 8 first-round workgroup groups of an XCD for `tile` = 14 (the 256x256 kernel with
- * staggered tile rounds), in 10 ns ticks. */
+ * staggered tile rounds), in 10 ns ticks; also the persistent kernel's group-M height for
+ * `tile` = 18. key 2: 0 turns the 3-stage pipeline of the two smallest tile configs off (A/B
+ * timing; both schedules give bitwise-equal results). */
 int echo_gemm_set_diag(int32_t key, int32_t value);
 
 /* One key/value segment of the joint attention (model.py:246-253): rows of

@@ -50,11 +50,14 @@ def main():
     ap.add_argument("--shapes", default=None, help="M,N,K[,epi];... overrides the production list")
     ap.add_argument("--pad-a", type=int, default=0, help="row stride of A = K + pad (elements)")
     ap.add_argument("--pad-c", type=int, default=0, help="row stride of the output = N + pad (elements)")
+    ap.add_argument("--no-ns3", action="store_true", help="2-stage pipeline for the small tiles (A/B)")
     ap.add_argument("--bias", action="store_true", help="add a bias vector (generic epilogue kind)")
     ap.add_argument("--stagger", type=int, default=0, help="tile 14: first-round group delay (10 ns ticks)")
     args = ap.parse_args()
     if args.stagger:
         assert L.load().echo_gemm_set_diag(1, args.stagger) == 0
+    if args.no_ns3:
+        assert L.load().echo_gemm_set_diag(2, 0) == 0
     shapes = SHAPES
     if args.shapes:
         shapes = []
