@@ -1250,9 +1250,11 @@ int pick_tile(int M, int N, int K, int batch) {
   // Under-filled launches (fewer tiles than CUs) are latency-bound per workgroup, which the
   // throughput model does not see: take the largest multi-block config that still gives every CU
   // a tile, else the one with the most tiles (tools/bench_gemm.py, e.g. M=1920 N=2048 K=5888:
-  // 256x128 86.7 us, 128x64 61.6 us; M=640 N=80: 39.7 -> 14.2 us on 64x64)
+  // 256x128 86.7 us, 128x64 61.6 us; M=640 N=80: 39.7 -> 14.2 us on 64x64). At half fill or more the
+  // big tile still wins (C5 decoder, N=2048 residual: M=7680 / 240 tiles 59.8 vs 74.5 us on 128x128,
+  // M=5120 / 160 tiles 48.3 vs 55.9 us; M=2560 / 80 tiles 45.3 vs 33.3 us): its switch is below 128
   auto ntiles = [&](int c) { return (double)((M + kTiles[c].bm - 1) / kTiles[c].bm) * ((N + kTiles[c].bn - 1) / kTiles[c].bn) * batch; };
-  if (ntiles(best - 1) < 256) {
+  if (ntiles(best - 1) < (best == 1 ? 128 : 256)) {
     for (int c = 2; c < 5; ++c)
       if (ntiles(c) >= 256 || c == 4) return c + 1;
   }

@@ -90,3 +90,14 @@ def test_model_refuses_cpu_device(lib):
     from echo_tts_amd.model import EchoDiTHip
     with pytest.raises(RuntimeError, match="HIP device only"):
         EchoDiTHip(E.tiny(), {}, device="cpu", dtype=torch.bfloat16)
+
+
+def test_gemm_tile_pick_host_policy(lib):
+    """The tile pick is host-only code (gemm.hip pick_tile): 256x256 (13) once half the CUs get a tile,
+    the smaller multi-block configs for the under-filled B=1 / plain-row decoder shapes."""
+    pick = lib.echo_gemm_pick_tile
+    assert pick(30720, 2048, 2048, 1) == 13  # C3 CFG residual
+    assert pick(7680, 2048, 5888, 1) == 13   # C5 CFG residual, 240 tiles
+    assert pick(5120, 2048, 2048, 1) == 13   # 160 tiles
+    assert pick(2560, 2048, 2048, 1) == 3    # 80 tiles -> 128x128
+    assert pick(1920, 2048, 5888, 1) == 4    # C2 CFG residual, 64 tiles -> 128x64
