@@ -1,7 +1,12 @@
-"""ctypes binding of the C ABI declared in `include/echo_hip.h`.
+"""Loading of the native libraries.
 
-This is the only place the shared library is loaded. If `libecho_hip.so` is
-missing the import fails loudly: the product path has no CPU fallback.
+* `libecho_hip.so` — the C ABI declared in `include/echo_hip.h`, bound here with
+  ctypes (ABI/layout tests, the Fish-S1-DAC codec kernels, diagnostics);
+* `libecho_torch.so` — `TORCH_LIBRARY(echo_hip)`: the sampling path's PyTorch
+  custom ops over that ABI (`load_torch_ops`, used by `ops.py`).
+
+If either library is missing the load fails loudly: the product path has no CPU
+fallback.
 """
 from __future__ import annotations
 
@@ -10,6 +15,7 @@ import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libecho_hip.so")
+TORCH_LIB_PATH = os.path.join(PKG, "libecho_torch.so")  # TORCH_LIBRARY(echo_hip) over the C ABI
 
 ECHO_BF16, ECHO_F32 = 0, 1
 EPI_STORE, EPI_SWIGLU, EPI_RESID, EPI_F32OUT, EPI_HEADNORM = 0, 1, 2, 3, 4
@@ -107,6 +113,23 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         fn.restype, fn.argtypes = res, args
     _lib = lib
     return lib
+
+
+_torch_loaded = False
+
+
+def load_torch_ops(path: str = TORCH_LIB_PATH):
+    """Register the `torch.ops.echo_hip.*` custom ops (csrc/torch_ops.cpp); raises if absent."""
+    global _torch_loaded
+    import torch
+    if not _torch_loaded:
+        load()
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} not found: build it with `python -c 'import __graft_entry__ as g; "
+                               f"g.build()'` (the HIP path has no CPU fallback)")
+        torch.ops.load_library(path)
+        _torch_loaded = True
+    return torch.ops.echo_hip
 
 
 def check(rc: int, what: str) -> None:

@@ -17,6 +17,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(PKG, "libecho_hip.so")
+TORCH_OUT = os.path.join(PKG, "libecho_torch.so")  # TORCH_LIBRARY(echo_hip) registration over the C ABI
 OBJ = os.path.join(PKG, "build")
 SOURCES = ["gemm.hip", "attention.hip", "elementwise.hip", "codec.hip"]
 HEADERS = [os.path.join(CSRC, "common.h"), os.path.join(REPO, "include", "echo_hip.h")]
@@ -36,6 +37,30 @@ def _stale(target: str, deps) -> bool:
         return True
     t = os.path.getmtime(target)
     return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_torch_ops(force: bool = False, verbose: bool = True) -> str:
+    """`libecho_torch.so`: the PyTorch custom ops (csrc/torch_ops.cpp), host C++ linked against
+    libecho_hip.so (rpath $ORIGIN) and the torch/c10 libraries of the running interpreter."""
+    import torch.utils.cpp_extension as ce
+    src = os.path.join(CSRC, "torch_ops.cpp")
+    if not (force or _stale(TORCH_OUT, [src, OUT] + HEADERS)):
+        return TORCH_OUT
+    import torch
+    inc = [f"-I{p}" for p in ce.include_paths()] + ["-I/opt/rocm/include", f"-I{os.path.join(REPO, 'include')}"]
+    libdir = ce.library_paths()[0]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    tmp = TORCH_OUT + ".tmp"
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-fPIC", "-std=c++17", "-shared", "-D__HIP_PLATFORM_AMD__=1",
+           "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", *inc, src, "-o", tmp, f"-L{libdir}", "-lc10",
+           "-lc10_hip", "-ltorch_cpu", f"-L{PKG}", "-lecho_hip", "-Wl,-rpath,$ORIGIN"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"torch op library failed:\n{r.stderr[-4000:]}")
+    os.replace(tmp, TORCH_OUT)
+    if verbose:
+        print(f"built {TORCH_OUT}")
+    return TORCH_OUT
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
@@ -69,6 +94,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
         os.replace(tmp, OUT)
         if verbose:
             print(f"built {OUT}")
+    build_torch_ops(force, verbose)
     return OUT
 
 

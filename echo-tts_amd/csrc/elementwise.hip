@@ -407,6 +407,6 @@ int echo_cast_from_f32(int32_t dtype, const float* x, void* y, int64_t n, void* 
   return 0;
 }
 
-const char* echo_version(void) { return "echo_hip gfx950 r1 " __DATE__ " " __TIME__; }
+const char* echo_version(void) { return "echo_hip gfx950 r2 " __DATE__ " " __TIME__; }
 
 }  // extern "C"

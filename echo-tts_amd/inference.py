@@ -4,7 +4,7 @@ Public names and signatures are the reference's:
   tokenizer_encode (:152-182), get_text_input_ids_and_mask (:185-217),
   ae_encode / ae_decode (:223-235), get_speaker_latent_and_mask (:250-309),
   find_flattening_point / crop_audio_to_flattening_point (:315-338),
-  SampleFn (:341-343), sample_pipeline (:346-400), KVCache (:406),
+  compile_model (:72-77), SampleFn (:341-343), sample_pipeline (:346-400), KVCache (:406),
   _concat_kv_caches (:409-417), _multiply_kv_cache (:420-428),
   _temporal_score_rescale (:431-443),
   sample_euler_cfg_independent_guidances (:446-560).
@@ -175,6 +175,21 @@ def sample_pipeline(model, fish_ae, pca_state: PCAState, sample_fn: SampleFn, te
     latent = sample_fn(model, spk, smask, ids, mask, rng_seed)
     audio = ae_decode(fish_ae, pca_state, latent)
     return crop_audio_to_flattening_point(audio, latent[0]), norm[0]
+
+
+def compile_model(model):
+    """`compile_model` (inference.py:72-77). For an `EchoDiTHip` the decoder body of `forward`
+    (`decoder_fn`) is compiled with `fullgraph=True`: every op on it is a registered
+    `torch.ops.echo_hip` custom op with a fake kernel, so the whole 24-layer decoder is one graph.
+    The KV-cache builders stay eager (their host-side mask checks run once per prompt), and the
+    engine path of the samplers keeps its own hipGraph, which replaces compilation there."""
+    if isinstance(model, EchoDiTHip):
+        model.decoder_fn = torch.compile(model.decoder_fn, fullgraph=True, dynamic=False)
+        return model
+    model = torch.compile(model)
+    for name in ("get_kv_cache_text", "get_kv_cache_speaker", "get_kv_cache_latent"):
+        setattr(model, name, torch.compile(getattr(model, name)))
+    return model
 
 
 # ---------------------------------------------------------------------------- sampler helpers

@@ -133,7 +133,7 @@ class EchoDiTHip:
 
     def __init__(self, cfg: EchoConfig, state: Dict[str, Tensor], device="cuda",
                  dtype: torch.dtype = torch.bfloat16):
-        L.load()  # fail loudly without the HIP library
+        ops.T()  # fail loudly without the HIP libraries (C ABI + torch.ops.echo_hip)
         cfg.check()
         if dtype not in (torch.bfloat16, torch.float32):
             raise TypeError("dtype must be bfloat16 or float32")
@@ -366,7 +366,7 @@ class EchoDiTHip:
             ops.gemm(a3, self.ada_up[ci], out=raw[:, :, ci, :], bias=self.ada_up_b[ci], epilogue=L.EPI_RESID,
                      aux=cc.unsqueeze(0).expand(n_ada, S, D))
         table = torch.empty((S, n_ada, 3, D), device=self._device, dtype=self._dtype)
-        ops.adaln_finish(raw, table, n_ada, S, D)
+        ops.adaln_finish(raw, table)
         return table
 
     # ------------------------------------------------------------------ decoder
@@ -392,7 +392,6 @@ class EchoDiTHip:
         q4 = ws.qkvg.view(R, N, 4, H, 128)
         self_seg = ops.Segment(q4[:, :, 1], q4[:, :, 2])
         og4 = ws.og.view(R, N, H, 128)
-        vstride = tab.stride(0) if per_row_tab else 0
         shared = None if callable(segs) else [self_seg] + [s for s in segs if s is not None]
         for i, lay in enumerate(self.layers):
             all_segs = shared if shared is not None else [self_seg] + [s for s in segs(i) if s is not None]
@@ -401,8 +400,7 @@ class EchoDiTHip:
                     sh, s1, g = tab[:, 2 * i + a, 0], tab[:, 2 * i + a, 1], tab[:, 2 * i + a, 2]
                 else:
                     sh, s1, g = tab[2 * i + a, 0], tab[2 * i + a, 1], tab[2 * i + a, 2]
-                ops.adaln_modulate(ws.h, sh, s1, eps, ws.xn, rows_per_vec=N if per_row_tab else 0,
-                                   vec_stride=vstride)
+                ops.adaln_modulate(ws.h, sh, s1, eps, ws.xn)
                 if a == 0:
                     # QKVG projection with q/k RMSNorm + half RoPE fused into its epilogue
                     ops.gemm(ws.xn, lay.wqkvg, out=ws.qkvg,
@@ -443,8 +441,8 @@ class EchoDiTHip:
             tab = tab.index_select(0, idx).contiguous()
         else:
             tab = tab[0]
-        ws = self.workspace(R * N)
-        ops.latent_to_input(x.detach().to(self._device).float().contiguous(), ws.xin, 1)
+        xin = torch.ops.echo_hip.latent_to_input(x.detach().to(self._device).float().contiguous(), 1, IN_PAD,
+                                                 self._dtype)
         dev = self._device
         t_lens = torch.tensor(prefix_lengths(text_mask), dtype=torch.int32).to(dev)
         s_lens = torch.tensor(prefix_lengths(speaker_mask[..., ::cfg.speaker_patch_size]), dtype=torch.int32).to(dev)
@@ -456,17 +454,55 @@ class EchoDiTHip:
             if kv_cache_latent is not None and kv_cache_latent[i][0].shape[1] > 0:
                 kl, vl = kv_cache_latent[i]
                 nval = min(kl.shape[1], -(-sp // cfg.speaker_patch_size))
-                lat = ops.Segment(*_pair(kl, vl), lens=torch.full((R,), nval, dtype=torch.int32, device=dev),
-                                  batch_mod=kl.shape[0])
-                if nval == 0:
-                    lat = None
-            segs_per_layer.append([
-                lat,
-                ops.Segment(*_pair(kt, vt), lens=t_lens, batch_mod=kt.shape[0]),
-                ops.Segment(*_pair(ks, vs), lens=s_lens, batch_mod=ks.shape[0]),
-            ])
-        v = self.decoder(ws, R, N, tab, lambda i: segs_per_layer[i], sp, per_row)
-        return v.view(R, N, C).clone()
+                if nval > 0:
+                    lat = (*_pair(kl, vl), torch.full((R,), nval, dtype=torch.int32, device=dev), kl.shape[0])
+            segs = [] if lat is None else [lat]
+            segs.append((*_pair(kt, vt), t_lens, kt.shape[0]))
+            segs.append((*_pair(ks, vs), s_lens, ks.shape[0]))
+            segs_per_layer.append(segs)
+        v = self.decoder_fn(xin, tab, segs_per_layer, R, N, sp)
+        return v.view(R, N, C)
+
+    def decoder_fn(self, xin: Tensor, tab: Tensor, segs_per_layer: Sequence[Sequence[Tuple]], R: int, N: int,
+                   start_pos: int = 0) -> Tensor:
+        """Functional form of `decoder` (model.py:575-604): every op allocates its output, nothing
+        is written in place — the form `compile_model` hands to torch.compile (fullgraph).
+
+        xin [R*N, 128] model dtype; tab [2L, 3, D] (one timestep) or [R, 2L, 3, D] (per row);
+        segs_per_layer[i] = [(k, v, lens int32 [R], batch_mod), ...] conditioning segments of layer i
+        (self-attention keys come from the layer's own projection). Returns v [R*N, 80] fp32."""
+        cfg = self.cfg
+        D, H, eps = cfg.model_size, cfg.num_heads, cfg.norm_eps
+        per_row = tab.dim() == 4
+        T = torch.ops.echo_hip
+        h = T.gemm(xin, self.w_in, self.b_in)
+        for i, lay in enumerate(self.layers):
+            seg_k = [None] + [s[0] for s in segs_per_layer[i]]
+            seg_v = [None] + [s[1] for s in segs_per_layer[i]]
+            seg_len = [None] + [s[2] for s in segs_per_layer[i]]
+            seg_bm = [0] + [int(s[3]) for s in segs_per_layer[i]]
+            causal = [0] * len(seg_bm)
+            for a in range(2):
+                t = tab[:, 2 * i + a] if per_row else tab[2 * i + a]
+                sh, s1, g = t[..., 0, :], t[..., 1, :], t[..., 2, :]
+                xn = T.norm_modulate(h, sh, s1, eps)
+                if a == 0:
+                    qkvg = T.gemm(xn, lay.wqkvg, hn_w=lay.qk_norm, hn_rope=self.rope,
+                                  hn=[H, 2, H * 128, H // 2, N, start_pos, 1], hn_eps=eps)
+                    q4 = qkvg.view(R, N, 4, H, 128)
+                    seg_k[0], seg_v[0] = q4[:, :, 1], q4[:, :, 2]
+                    src = T.joint_attention(q4[:, :, 0], q4[:, :, 3], seg_k, seg_v, seg_len, seg_bm, causal)
+                    w = lay.wo
+                else:
+                    src = T.gemm(xn, lay.w13, epilogue=L.EPI_SWIGLU)
+                    w = lay.w2
+                if per_row:
+                    h = T.gemm(src.view(R, N, -1), w, epilogue=L.EPI_RESID, aux=h.view(R, N, D),
+                               gate=g).view(R * N, D)
+                else:
+                    h = T.gemm(src.view(R * N, -1), w, epilogue=L.EPI_RESID, aux=h, gate=g)
+        xn = T.rmsnorm(h, self.out_norm, eps)
+        return T.gemm(xn, self.w_out, self.b_out, L.EPI_F32OUT)
 
 
 def _pair(k: Tensor, v: Tensor) -> Tuple[Tensor, Tensor]:

@@ -101,3 +101,58 @@ def test_gemm_tile_pick_host_policy(lib):
     assert pick(5120, 2048, 2048, 1) == 13   # 160 tiles
     assert pick(2560, 2048, 2048, 1) == 3    # 80 tiles -> 128x128
     assert pick(1920, 2048, 5888, 1) == 4    # C2 CFG residual, 64 tiles -> 128x64
+
+
+TORCH_OPS = ("gemm", "gemm_out", "joint_attention", "joint_attention_out", "attention_variant_out", "rmsnorm",
+             "rmsnorm_out", "norm_modulate", "norm_modulate_out", "head_norm_rope_", "timestep_embedding", "silu",
+             "silu_out", "adaln_finish", "adaln_finish_out", "latent_to_input", "latent_to_input_out",
+             "euler_cfg_step", "euler_cfg_step_", "embed", "embed_out", "scale_rows_", "cast_from_f32",
+             "cast_from_f32_out", "gemm_pick_tile", "version")
+
+
+def test_torch_ops_registered(lib):
+    """TORCH_LIBRARY(echo_hip) (csrc/torch_ops.cpp) loads without a GPU and registers every op of the
+    sampling path; CPU tensors are refused loudly (no CPU fallback); host-only ops answer."""
+    import torch
+    from echo_tts_amd import ops
+    T = ops.T()
+    for name in TORCH_OPS:
+        assert hasattr(T, name), name
+    assert T.version().startswith("echo_hip gfx950")
+    assert T.gemm_pick_tile(30720, 2048, 2048, 1) == lib.echo_gemm_pick_tile(30720, 2048, 2048, 1)
+    a = torch.zeros(4, 64, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        T.gemm(a, a)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        T.rmsnorm(a, a[0], 1e-5)
+
+
+def test_torch_ops_fake_kernels():
+    """Every functional op has a fake (meta) kernel: shapes/dtypes under FakeTensorMode on CPU."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    from echo_tts_amd import ops
+    T = ops.T()
+    bf = torch.bfloat16
+    with FakeTensorMode():
+        a = torch.empty(640, 2048, dtype=bf, device="cuda")
+        assert T.gemm(a, torch.empty(11776, 2048, dtype=bf, device="cuda"), epilogue=L.EPI_SWIGLU).shape == (640, 5888)
+        o = T.gemm(a, torch.empty(80, 2048, dtype=bf, device="cuda"), epilogue=L.EPI_F32OUT)
+        assert o.shape == (640, 80) and o.dtype == torch.float32
+        b3 = T.gemm(torch.empty(3, 640, 2048, dtype=bf, device="cuda"), torch.empty(256, 2048, dtype=bf, device="cuda"))
+        assert b3.shape == (3, 640, 256)
+        q = torch.empty(3, 640, 16, 128, dtype=bf, device="cuda")
+        assert T.joint_attention(q, q, [q], [q], [None], [0], [0]).shape == q.shape
+        assert T.norm_modulate(a, a[0], a[0], 1e-5).shape == a.shape
+        assert T.rmsnorm(a, a[0], 1e-5).shape == a.shape
+        raw = torch.empty(48, 40, 3, 2048, dtype=bf, device="cuda")
+        assert T.adaln_finish(raw).shape == (40, 48, 3, 2048)
+        x = torch.empty(2, 640, 80, device="cuda")
+        l2i = T.latent_to_input(x, 3, 128, bf)
+        assert l2i.shape == (3 * 1280, 128) and l2i.dtype == bf
+        assert T.euler_cfg_step(x, torch.empty(3, 2, 640, 80, device="cuda"), 1, 3.0, 8.0, 0, 0., 0., 0., -0.02).shape == x.shape
+        ids = torch.empty(2, 17, dtype=torch.int32, device="cuda")
+        assert T.embed(ids, torch.empty(256, 128, dtype=bf, device="cuda")).shape == (34, 128)
+        assert T.cast_from_f32(x, bf).dtype == bf
+        assert T.timestep_embedding(torch.empty(40, device="cuda"), torch.empty(256, device="cuda"), bf).shape == (40, 512)
+        assert T.silu(a).shape == a.shape
