@@ -18,7 +18,7 @@ import torch
 
 from . import _lib as L
 from . import ops
-from .model import EchoDiTHip, KVStore, Workspace
+from .model import EchoDiTHip, KVStore, Workspace, prefix_lengths
 
 INIT_SCALE = 0.999  # inference.py:470
 
@@ -64,6 +64,19 @@ def round_up(v: int, m: int) -> int:
     return (v + m - 1) // m * m
 
 
+def caps(model: EchoDiTHip, text_input_ids, text_mask, speaker_latent, speaker_mask) -> Tuple[int, int]:
+    """Encoded text / speaker-patch capacities of a call: the longest valid prefix rounded up to
+    64 / 16 (positions past it are masked for every query, and the encoders are per-row /
+    causal, so results are unchanged), at most the given lengths; Pc = 0 without speaker."""
+    t_lens = prefix_lengths(text_mask)
+    Tc = min(text_input_ids.shape[1], round_up(max(t_lens), 64))
+    ps = model.cfg.speaker_patch_size
+    s_valid = prefix_lengths(speaker_mask[..., ::ps])
+    P = speaker_latent.shape[1] // ps
+    Pc = 0 if max(s_valid) == 0 else min(P, round_up(max(s_valid), 16))
+    return Tc, Pc
+
+
 def kv_scale_cols(model: EchoDiTHip, max_layers: Optional[int]) -> int:
     """Leading columns of a [tokens, L*2*D] KV row covered by the first `max_layers` layers."""
     nl = model.cfg.num_layers if max_layers is None else min(max_layers, model.cfg.num_layers)
@@ -93,7 +106,9 @@ class CFGPlan:
         self.runs = 0
 
     # -- per call
-    def setup(self, ids, text_mask, speaker_latent, speaker_mask, noise, truncation_factor):
+    def _setup_cond(self, ids, text_mask, speaker_latent, speaker_mask, prescale: bool):
+        """Text / speaker KV caches (encoders + stacked K/V projections), per-row valid lengths and
+        the per-schedule AdaLN table (inference.py:478-497)."""
         m, B = self.m, self.B
         kt = m.text_kv(ids, text_mask, trim=True, cap=self.Tc, out=self.kv_text)
         if kt.capacity != self.Tc:
@@ -101,7 +116,7 @@ class CFGPlan:
         if self.Pc > 0:
             ks = m.speaker_kv(speaker_latent, speaker_mask, trim=True, cap=self.Pc, out=self.kv_spk)
             s_lens = ks.lens
-            if self.kv_scale is not None:
+            if prescale and self.kv_scale is not None:
                 self._scale_speaker(self.kv_scale)
         else:
             s_lens = [0] * B
@@ -113,6 +128,9 @@ class CFGPlan:
         host[3, :B] = torch.tensor(s_lens, dtype=torch.int32)
         self.lens.copy_(host.to(self.lens.device, non_blocking=False))
         self.table.copy_(m.adaln_table(self.sched.t[:-1]))
+
+    def setup(self, ids, text_mask, speaker_latent, speaker_mask, noise, truncation_factor):
+        self._setup_cond(ids, text_mask, speaker_latent, speaker_mask, prescale=True)
         self.x.copy_(noise)
         if truncation_factor is not None:
             ops.scale_rows(self.x.view(-1, self.x.shape[-1]), self.x.shape[-1], float(truncation_factor))
@@ -134,20 +152,24 @@ class CFGPlan:
             return [None, t, s]
         return per_layer
 
+    def _step(self, i: int, x: torch.Tensor, N: int, segs_cfg, segs_plain, start_pos: int = 0):
+        """One Euler step (inference.py:508-558): x fp32 [B, N, 80] -> model input (x3 for CFG),
+        decoder, fused CFG combine + rescale + Euler update in place."""
+        cfg_step = self.sched.has_cfg[i]
+        copies = 3 if cfg_step else 1
+        ws = self.ws.view(copies * self.B * N)
+        ops.latent_to_input(x, ws.xin, copies)
+        self.m.decoder(ws, copies * self.B, N, self.table[i], segs_cfg if cfg_step else segs_plain, start_pos)
+        ops.euler_step(x, ws.v, self.args[i])
+        if self.sched.unscale_step == i and self.kv_scale is not None:
+            self._scale_speaker(1.0 / self.kv_scale)
+        return ws.v
+
     # -- the capturable step loop (inference.py:508-558)
     def loop(self):
-        m, B, N = self.m, self.B, self.N
         seg_cfg, seg_plain = self._segs(True), self._segs(False)
         for i in range(self.sched.steps):
-            cfg_step = self.sched.has_cfg[i]
-            copies = 3 if cfg_step else 1
-            R = copies * B
-            ws = self.ws.view(R * N)
-            ops.latent_to_input(self.x, ws.xin, copies)
-            m.decoder(ws, R, N, self.table[i], seg_cfg if cfg_step else seg_plain, 0)
-            ops.euler_step(self.x, ws.v, self.args[i])
-            if self.sched.unscale_step == i and self.kv_scale is not None:
-                self._scale_speaker(1.0 / self.kv_scale)
+            self._step(i, self.x, self.N, seg_cfg, seg_plain)
 
     def run(self, use_graph: bool) -> torch.Tensor:
         """Eager on the first call (this also loads every kernel before any capture),
@@ -164,17 +186,146 @@ class CFGPlan:
         self.runs += 1
         return self.x
 
+    @torch.no_grad()
+    def nfe(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        """Teacher-forced evaluation (tests): the model output of step i on the given state x
+        [B, N, 80] with this plan's production buffers, caches and kernels (eager; the state and
+        the speaker-KV scale are left as they were). Returns v [copies*B, N, 80] fp32."""
+        if self.kv_scale is not None and self.sched.unscale_step is not None and i > self.sched.unscale_step:
+            raise ValueError("nfe() evaluates with the speaker KV as setup() left it (scaled)")
+        xs = x.to(self.x.device, torch.float32).contiguous()
+        copies = 3 if self.sched.has_cfg[i] else 1
+        ws = self.ws.view(copies * self.B * self.N)
+        ops.latent_to_input(xs, ws.xin, copies)
+        seg = self._segs(self.sched.has_cfg[i])
+        self.m.decoder(ws, copies * self.B, self.N, self.table[i], seg, 0)
+        return ws.v.view(copies * self.B, self.N, -1).clone()
+
+
+class BlockPlan(CFGPlan):
+    """The blockwise sampler (inference_blockwise.py:14-123) as ONE hipGraph per call: for every
+    block the latent-prefix encoder + stacked K/V projection of the visible patches, the per-block
+    speaker-KV scale (and its un-scale when t crosses speaker_kv_min_t), the block's Euler steps
+    with start_pos and the latent segment, and the write-back into the prefix.
+
+    Each block's x_T is drawn in `setup`, in the reference's order and shapes, from the same
+    generator (nothing else draws between the blocks), so the captured graph needs no RNG."""
+
+    @torch.inference_mode(False)
+    def __init__(self, model: EchoDiTHip, B: int, blocks: Tuple[int, ...], start0: int, Tc: int, Pc: int,
+                 sched: Schedule, kv_scale: Optional[float], kv_max_layers: Optional[int]):
+        super().__init__(model, B, max(blocks), Tc, Pc, sched, kv_scale, kv_max_layers)
+        if not model.has_latent:
+            raise RuntimeError("model was built without the blockwise (latent) modules")
+        cfg = model.cfg
+        dev, C, ps = model.device, cfg.latent_size, cfg.speaker_patch_size
+        self.blocks, self.start0 = tuple(blocks), start0
+        self.total = start0 + sum(blocks)
+        self.prefix = torch.zeros((B, self.total, C), device=dev, dtype=torch.float32)
+        self.noise = [torch.empty((B, bs, C), device=dev, dtype=torch.float32) for bs in blocks]
+        self.xb = [torch.empty((B, bs, C), device=dev, dtype=torch.float32) for bs in blocks]
+        self.starts, self.nval, self.lat_lens = [], [], []
+        st = start0
+        for bs in blocks:
+            nv = min(-(-st // ps), self.total // ps)   # patches j with 4j < start_pos (model.py:243-244)
+            self.starts.append(st)
+            self.nval.append(nv)
+            self.lat_lens.append(torch.full((3 * B,), nv, device=dev, dtype=torch.int32))
+            st += bs
+
+    def setup(self, ids, text_mask, speaker_latent, speaker_mask, noise_fn, truncation_factor,
+              continuation=None):
+        self._setup_cond(ids, text_mask, speaker_latent, speaker_mask, prescale=False)
+        self.prefix.zero_()
+        if continuation is not None:
+            self.prefix[:, :self.start0].copy_(continuation)
+        for buf, bs in zip(self.noise, self.blocks):
+            buf.copy_(noise_fn((self.B, bs, self.m.cfg.latent_size)))
+            if truncation_factor is not None:
+                ops.scale_rows(buf.view(-1, buf.shape[-1]), buf.shape[-1], float(truncation_factor))
+
+    def _block_segs(self, b: int, kl):
+        B = self.B
+        base_cfg, base_plain = self._segs(True), self._segs(False)
+
+        def wrap(base):
+            def f(i):
+                segs = base(i)
+                if kl.buf is not None:
+                    k, v = kl.layer(i)
+                    segs[0] = ops.Segment(k, v, lens=self.lat_lens[b], batch_mod=B)
+                return segs
+            return f
+        return wrap(base_cfg), wrap(base_plain)
+
+    def _latent_kv(self, b: int):
+        return self.m.latent_kv(self.prefix, valid_patches=self.nval[b], trim=True)
+
+    def loop(self):
+        for b, bs in enumerate(self.blocks):
+            if self.kv_scale is not None:
+                self._scale_speaker(self.kv_scale)  # re-applied every block (inference_blockwise.py:68-70)
+            kl = self._latent_kv(b)
+            seg_cfg, seg_plain = self._block_segs(b, kl)
+            x = self.xb[b]
+            x.copy_(self.noise[b])
+            for i in range(self.sched.steps):
+                self._step(i, x, bs, seg_cfg, seg_plain, self.starts[b])
+            self.prefix[:, self.starts[b]:self.starts[b] + bs].copy_(x)
+
+    def run(self, use_graph: bool) -> torch.Tensor:
+        super().run(use_graph)
+        return self.prefix
+
+    @torch.no_grad()
+    def nfe(self, b: int, i: int, x: torch.Tensor, prefix: torch.Tensor) -> torch.Tensor:
+        """Teacher-forced step i of block b (tests): the given state x [B, bs, 80] and prefix
+        [B, total, 80] (positions >= the block start are zeroed as in the reference), the speaker-KV
+        scale chain the call would have applied by then, this plan's buffers and kernels.
+        Call right after `setup`; leaves the speaker KV re-scaled (call setup again to reset)."""
+        self.prefix.copy_(prefix)
+        self.prefix[:, self.starts[b]:].zero_()
+        if self.kv_scale is not None:
+            for _ in range(b):
+                self._scale_speaker(self.kv_scale)
+                if self.sched.unscale_step is not None:
+                    self._scale_speaker(1.0 / self.kv_scale)
+            self._scale_speaker(self.kv_scale)
+            if self.sched.unscale_step is not None and i > self.sched.unscale_step:
+                self._scale_speaker(1.0 / self.kv_scale)
+        kl = self._latent_kv(b)
+        seg_cfg, seg_plain = self._block_segs(b, kl)
+        bs = self.blocks[b]
+        xs = x.to(self.prefix.device, torch.float32).contiguous()
+        copies = 3 if self.sched.has_cfg[i] else 1
+        ws = self.ws.view(copies * self.B * bs)
+        ops.latent_to_input(xs, ws.xin, copies)
+        self.m.decoder(ws, copies * self.B, bs, self.table[i], seg_cfg if self.sched.has_cfg[i] else seg_plain,
+                       self.starts[b])
+        return ws.v.view(copies * self.B, bs, -1).clone()
+
 
 def plan_key(B, N, Tc, Pc, sched: Schedule, kv_scale, kv_max_layers):
     return (B, N, Tc, Pc, sched, kv_scale, kv_max_layers)
 
 
-def get_plan(model: EchoDiTHip, B: int, N: int, Tc: int, Pc: int, sched: Schedule,
-             kv_scale: Optional[float], kv_max_layers: Optional[int]) -> CFGPlan:
+def _cached(model: EchoDiTHip, key, make):
     cache = model.__dict__.setdefault("_plans", {})
-    key = plan_key(B, N, Tc, Pc, sched, kv_scale, kv_max_layers)
     if key not in cache:
         if len(cache) >= 4:
             cache.pop(next(iter(cache)))
-        cache[key] = CFGPlan(model, B, N, Tc, Pc, sched, kv_scale, kv_max_layers)
+        cache[key] = make()
     return cache[key]
+
+
+def get_plan(model: EchoDiTHip, B: int, N: int, Tc: int, Pc: int, sched: Schedule,
+             kv_scale: Optional[float], kv_max_layers: Optional[int]) -> CFGPlan:
+    return _cached(model, plan_key(B, N, Tc, Pc, sched, kv_scale, kv_max_layers),
+                   lambda: CFGPlan(model, B, N, Tc, Pc, sched, kv_scale, kv_max_layers))
+
+
+def get_block_plan(model: EchoDiTHip, B: int, blocks, start0: int, Tc: int, Pc: int, sched: Schedule,
+                   kv_scale: Optional[float], kv_max_layers: Optional[int]) -> BlockPlan:
+    key = ("blockwise", tuple(blocks), start0) + plan_key(B, max(blocks), Tc, Pc, sched, kv_scale, kv_max_layers)
+    return _cached(model, key, lambda: BlockPlan(model, B, tuple(blocks), start0, Tc, Pc, sched, kv_scale,
+                                                 kv_max_layers))

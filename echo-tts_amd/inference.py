@@ -27,7 +27,7 @@ from typing import Callable, List, Optional, Tuple
 import torch
 
 from . import engine as E
-from .model import EchoDiTHip, prefix_lengths
+from .model import EchoDiTHip
 
 KVCache = List[Tuple[torch.Tensor, torch.Tensor]]
 
@@ -253,17 +253,10 @@ def sample_with_noise(model, speaker_latent, speaker_mask, text_input_ids, text_
         return _generic_loop(model, speaker_latent, speaker_mask, text_input_ids, text_mask, noise, num_steps,
                              cfg_scale_text, cfg_scale_speaker, cfg_min_t, cfg_max_t, truncation_factor,
                              rescale_k, rescale_sigma, speaker_kv_scale, speaker_kv_max_layers, speaker_kv_min_t)
-    cfgm = model.cfg
     B, N = noise.shape[0], noise.shape[1]
     sched = E.make_schedule(num_steps, cfg_scale_text, cfg_scale_speaker, cfg_min_t, cfg_max_t, rescale_k,
                             rescale_sigma, speaker_kv_scale, speaker_kv_min_t)
-    t_lens = prefix_lengths(text_mask)
-    T = text_input_ids.shape[1]
-    Tc = min(T, E.round_up(max(t_lens), 64))
-    ps = cfgm.speaker_patch_size
-    s_valid = prefix_lengths(speaker_mask[..., ::ps])
-    P = speaker_latent.shape[1] // ps
-    Pc = 0 if max(s_valid) == 0 else min(P, E.round_up(max(s_valid), 16))
+    Tc, Pc = E.caps(model, text_input_ids, text_mask, speaker_latent, speaker_mask)
     plan = E.get_plan(model, B, N, Tc, Pc, sched, speaker_kv_scale, speaker_kv_max_layers)
     plan.setup(text_input_ids, text_mask, speaker_latent, speaker_mask, noise.to(model.device, torch.float32),
                truncation_factor)

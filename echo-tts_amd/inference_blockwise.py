@@ -1,9 +1,11 @@
 """Drop-in mirror of `/root/reference/inference_blockwise.py:14-123` (blockwise /
 continuation sampler, BASELINE config 5).
 
-With an `EchoDiTHip` model each block runs the same decoder as the CFG engine
-with `start_pos` and a latent-prefix KV segment. Differences from the reference
-that do not change results:
+With an `EchoDiTHip` model the call runs as `engine.BlockPlan`: every block's
+latent-prefix encoder, speaker-KV scale/un-scale and 40 Euler steps (the same
+decoder as the CFG engine, with `start_pos` and a latent-prefix KV segment) are
+captured once as ONE hipGraph and replayed. Differences from the reference that
+do not change results:
   * the latent encoder runs on the B distinct prefixes instead of the 3B
     replicated copies (rows are identical), and only on the patches the decoder
     can see (j with 4j < start_pos; the encoder is causal, so this is exact);
@@ -16,7 +18,6 @@ from typing import Callable, List, Optional
 import torch
 
 from . import engine as E
-from . import ops
 from .inference import _concat_kv_caches, _multiply_kv_cache, _temporal_score_rescale
 from .model import EchoDiTHip
 
@@ -49,72 +50,23 @@ def blockwise_with_noise(model, speaker_latent, speaker_mask, text_input_ids, te
                          noise: Callable[[tuple], torch.Tensor], block_sizes: List[int], *, num_steps,
                          cfg_scale_text, cfg_scale_speaker, cfg_min_t, cfg_max_t, truncation_factor=None,
                          rescale_k=None, rescale_sigma=None, speaker_kv_scale=None, speaker_kv_max_layers=None,
-                         speaker_kv_min_t=None, continuation_latent=None) -> torch.Tensor:
-    """Blockwise sampler body; `noise(shape)` supplies each block's x_T in order."""
+                         speaker_kv_min_t=None, continuation_latent=None, use_graph: bool = True) -> torch.Tensor:
+    """Blockwise sampler body; `noise(shape)` supplies each block's x_T in order.
+    With an `EchoDiTHip` the whole call (all blocks) replays as one hipGraph (engine.BlockPlan)."""
     if not isinstance(model, EchoDiTHip):
         return _generic_blockwise(model, speaker_latent, speaker_mask, text_input_ids, text_mask, noise,
                                   block_sizes, num_steps, cfg_scale_text, cfg_scale_speaker, cfg_min_t, cfg_max_t,
                                   truncation_factor, rescale_k, rescale_sigma, speaker_kv_scale,
                                   speaker_kv_max_layers, speaker_kv_min_t, continuation_latent)
-    m, cfg = model, model.cfg
-    dev = m.device
-    B = text_input_ids.shape[0]
-    ps = cfg.speaker_patch_size
     sched = E.make_schedule(num_steps, cfg_scale_text, cfg_scale_speaker, cfg_min_t, cfg_max_t, rescale_k,
                             rescale_sigma, speaker_kv_scale, speaker_kv_min_t)
-    args = [E.step_args(a) for a in sched.args]
-    kt = m.text_kv(text_input_ids, text_mask, trim=True)
-    ks = m.speaker_kv(speaker_latent, speaker_mask, trim=True)
-    kv_cols = E.kv_scale_cols(m, speaker_kv_max_layers)
-    lens = torch.tensor([kt.lens + [0] * B + kt.lens, ks.lens + ks.lens + [0] * B, kt.lens + [0] * 2 * B,
-                         ks.lens + [0] * 2 * B], dtype=torch.int32).to(dev)
-    table = m.adaln_table(sched.t[:-1])
-    prefix = torch.zeros((B, sum(block_sizes), cfg.latent_size), device=dev, dtype=torch.float32)
-    start = 0
-    if continuation_latent is not None:
-        prefix = torch.cat([continuation_latent.to(dev, torch.float32), prefix], 1)
-        start = continuation_latent.shape[1]
-    ws_all = m.workspace(3 * B * max(block_sizes))
-
-    def scale_speaker(s):
-        if ks.buf is not None:
-            ops.scale_rows(ks.buf.view(B * ks.capacity, -1), kv_cols, float(s))
-
-    for bs in block_sizes:
-        if speaker_kv_scale is not None:
-            scale_speaker(speaker_kv_scale)  # re-applied every block (inference_blockwise.py:68-70)
-        nval = -(-start // ps)
-        kl = m.latent_kv(prefix, valid_patches=min(nval, prefix.shape[1] // ps), trim=True)
-        lat_len = torch.full((3 * B,), min(nval, kl.capacity), dtype=torch.int32, device=dev)
-
-        def segs_for(cfg_step):
-            i0 = 0 if cfg_step else 2
-
-            def f(i):
-                lat = None
-                if kl.buf is not None:
-                    lat = ops.Segment(*kl.layer(i), lens=lat_len, batch_mod=B)
-                t = ops.Segment(*kt.layer(i), lens=lens[i0], batch_mod=B)
-                s = ops.Segment(*ks.layer(i), lens=lens[i0 + 1], batch_mod=B) if ks.buf is not None else None
-                return [lat, t, s]
-            return f
-
-        seg_cfg, seg_plain = segs_for(True), segs_for(False)
-        x = noise((B, bs, cfg.latent_size)).to(dev, torch.float32).contiguous()
-        if truncation_factor is not None:
-            ops.scale_rows(x.view(-1, x.shape[-1]), x.shape[-1], float(truncation_factor))
-        for i in range(num_steps):
-            c = sched.has_cfg[i]
-            copies = 3 if c else 1
-            ws = ws_all.view(copies * B * bs)
-            ops.latent_to_input(x, ws.xin, copies)
-            m.decoder(ws, copies * B, bs, table[i], seg_cfg if c else seg_plain, start)
-            ops.euler_step(x, ws.v, args[i])
-            if sched.unscale_step == i and speaker_kv_scale is not None:
-                scale_speaker(1.0 / speaker_kv_scale)
-        prefix[:, start:start + bs] = x
-        start += bs
-    return prefix
+    B = text_input_ids.shape[0]
+    Tc, Pc = E.caps(model, text_input_ids, text_mask, speaker_latent, speaker_mask)
+    start0 = 0 if continuation_latent is None else continuation_latent.shape[1]
+    plan = E.get_block_plan(model, B, block_sizes, start0, Tc, Pc, sched, speaker_kv_scale, speaker_kv_max_layers)
+    cont = None if continuation_latent is None else continuation_latent.to(model.device, torch.float32)
+    plan.setup(text_input_ids, text_mask, speaker_latent, speaker_mask, noise, truncation_factor, cont)
+    return plan.run(use_graph).clone()
 
 
 def _generic_blockwise(model, speaker_latent, speaker_mask, text_input_ids, text_mask, noise, block_sizes,

@@ -1,5 +1,7 @@
-"""Multi-process path of bench.py on CPU (gloo, world size 2): per-rank prompt shards,
-the single all-gather of finished latents, and the max-over-ranks timing."""
+"""Multi-process sampling plumbing on CPU (gloo, world size 2 and 3): contiguous, possibly uneven
+prompt shards (`distributed.shard_range`), the single padded all-gather of finished rows
+(`distributed.gather_rows`), the reference's noise semantics (rows of ONE global draw), and
+bench.py's max-over-ranks timing."""
 import os
 import socket
 
@@ -10,6 +12,9 @@ import torch.multiprocessing as mp
 
 from conftest import REPO
 
+import echo_tts_amd  # noqa: F401
+from echo_tts_amd import distributed as D
+
 
 def _free_port():
     s = socket.socket()
@@ -19,44 +24,55 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+@pytest.mark.parametrize("batch,world", [(16, 8), (128, 8), (5, 2), (3, 4), (7, 3), (0, 2)])
+def test_shard_range_partitions_the_batch(batch, world):
+    ranges = [D.shard_range(batch, world, r) for r in range(world)]
+    assert ranges[0][0] == 0 and ranges[-1][1] == batch
+    for (s0, e0), (s1, _) in zip(ranges, ranges[1:]):
+        assert e0 == s1
+    sizes = [e - s for s, e in ranges]
+    assert max(sizes) - min(sizes) <= 1 and sizes == sorted(sizes, reverse=True)
+
+
+def _worker(rank, world, port, batch, q):
     import sys
     sys.path.insert(0, REPO)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
-    B = 2
-    ids, tm, spk, sm = bench.shard_inputs(rank, B)
-    # stand-in for this rank's sampler output: deterministic in the shard's inputs
-    lat = (spk[:, :4, :].sum(-1, keepdim=True) + ids[:, :4, None].float()).expand(B, 4, 80).contiguous()
-    out = torch.empty(world * B, 4, 80)
-    bench.gather_latents(dist, lat, out)
+    ids, tm, spk, sm = bench.global_inputs(batch)
+    s, e = D.shard_range(batch, world, rank)
+    # the reference's x_T: one draw of the whole batch, this rank keeps its rows
+    noise = torch.randn((batch, 4, 80), generator=torch.Generator().manual_seed(0))[s:e]
+    # stand-in for this rank's sampler output: deterministic in the shard's inputs and noise
+    lat = noise + spk[s:e, :4, :] + ids[s:e, :4, None].float()
+    out = D.gather_rows(lat, batch)
     t = bench.max_over_ranks(dist, 1.0 + rank, torch.device("cpu"))
-    q.put((rank, out, t, ids))
+    q.put((rank, out, t))
     dist.destroy_process_group()
 
 
-def test_two_rank_shards_and_gather():
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world,batch", [(2, 4), (3, 7)])
+def test_shards_and_gather(world, batch):
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, batch, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
     for _ in range(world):
-        r, out, t, ids = q.get(timeout=120)
-        res[r] = (out, t, ids)
+        r, out, t = q.get(timeout=120)
+        res[r] = (out, t)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     import sys
     sys.path.insert(0, REPO)
     import bench
-    # every rank holds the same gathered tensor, equal to the concatenation of the shards
-    assert torch.equal(res[0][0], res[1][0])
-    full_ids, _, full_spk, _ = bench.shard_inputs(0, 4)  # the global batch of 4 prompts
-    assert torch.equal(torch.cat([res[0][2], res[1][2]]), full_ids)
-    expect = (full_spk[:, :4, :].sum(-1, keepdim=True) + full_ids[:, :4, None].float()).expand(4, 4, 80)
-    assert torch.equal(res[0][0], expect)
-    assert res[0][1] == res[1][1] == 2.0
+    ids, _, spk, _ = bench.global_inputs(batch)
+    noise = torch.randn((batch, 4, 80), generator=torch.Generator().manual_seed(0))
+    expect = noise + spk[:, :4, :] + ids[:, :4, None].float()
+    for r in range(world):
+        assert torch.equal(res[r][0], expect)  # every rank holds the global batch, in prompt order
+        assert res[r][1] == float(world)       # max over ranks

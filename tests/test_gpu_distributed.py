@@ -1,8 +1,10 @@
-"""Multi-process sampling on the GPU: two ranks, each running the
-HIP sampler on its contiguous prompt shard, gather the finished latents with bench.py's
-collective (gloo here: one GPU box; RCCL on the driver's 8-GPU node), and the gathered batch
-equals a single-process run over the whole batch. Rows never interact (GEMM accumulation order
-does not depend on M, attention/norms are per row), so the check is bitwise."""
+"""Multi-process sampling on the GPU through the library (`echo_tts_amd.distributed`, SURVEY.md
+§8(e)): two ranks call the sharded samplers with the GLOBAL batch and the same seed; each samples
+its contiguous prompts (uneven split: 3 prompts over 2 ranks) with the rows of the single global
+x_T draw from the DEVICE generator, and the gathered batch is bitwise equal to one process running
+the public sampler over the whole batch — the reference's noise semantics
+(`/root/reference/inference.py:499-504`, `inference_blockwise.py:76-77`). One GPU box: both ranks
+share the card and gather over gloo; the driver's 8-GPU node uses RCCL."""
 import os
 import socket
 
@@ -15,8 +17,12 @@ from conftest import REPO
 
 pytestmark = pytest.mark.gpu
 
-B, N, T, S = 2, 96, 128, 64
-KW = dict(num_steps=4, cfg_scale_text=3.0, cfg_scale_speaker=8.0, cfg_min_t=0.5, cfg_max_t=1.0)
+BT, N, T, S = 3, 96, 128, 64
+KW = dict(num_steps=4, cfg_scale_text=3.0, cfg_scale_speaker=8.0, cfg_min_t=0.5, cfg_max_t=1.0,
+          truncation_factor=None, rescale_k=None, rescale_sigma=None, speaker_kv_scale=None,
+          speaker_kv_max_layers=None, speaker_kv_min_t=None)
+KW_BLK = dict(KW, speaker_kv_scale=1.5, speaker_kv_min_t=0.9, speaker_kv_max_layers=2)
+BLOCKS = [16, 24]
 
 
 def _free_port():
@@ -27,15 +33,13 @@ def _free_port():
     return p
 
 
-def _inputs(rank, batch):
+def _inputs():
     from echo_tts_amd import synthetic as SY
-    ids, tm = SY.text_inputs(batch, T=T, valid=60 + 7 * rank, first_seed=1000 + rank * B)
-    spk, sm = SY.speaker_inputs(batch, S=S, first_seed=2000 + rank * B)
-    return ids, tm, spk, sm
-
-
-def _noise(world):
-    return torch.randn((world * B, N, 80), generator=torch.Generator().manual_seed(7))
+    ids, tm = SY.text_inputs(BT, T=T, valid=60)
+    tm[1, 71:] = False
+    tm[1, 60:71] = True
+    spk, sm = SY.speaker_inputs(BT, S=S)
+    return tuple(t.to("cuda:0") for t in (ids, tm, spk, sm))
 
 
 def _model():
@@ -47,42 +51,42 @@ def _model():
                       dtype=torch.bfloat16)
 
 
-def _sample(m, ids, tm, spk, sm, noise):
-    from echo_tts_amd.inference import sample_with_noise
-    dev = "cuda:0"
-    return sample_with_noise(m, spk.to(dev), sm.to(dev), ids.to(dev), tm.to(dev), noise.to(dev), **KW)
-
-
 def _worker(rank, world, port, q):
     import sys
     sys.path.insert(0, REPO)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    import bench
+    from echo_tts_amd import distributed as D
     torch.cuda.set_device(0)
-    ids, tm, spk, sm = _inputs(rank, B)
-    lat = _sample(_model(), ids, tm, spk, sm, _noise(world)[rank * B:(rank + 1) * B]).cpu()
-    out = torch.empty(world * B, N, 80)
-    bench.gather_latents(dist, lat, out)
-    q.put((rank, out))
+    m = _model()
+    ids, tm, spk, sm = _inputs()
+    lat = D.sample_euler_cfg_sharded(m, spk, sm, ids, tm, 11, sequence_length=N, **KW).cpu()
+    blk = D.sample_blockwise_sharded(m, spk, sm, ids, tm, 12, BLOCKS, **KW_BLK).cpu()
+    q.put((rank, lat, blk))
     dist.destroy_process_group()
 
 
-def test_two_rank_hip_sampler_matches_single_process():
+def test_two_rank_sharded_samplers_match_single_process():
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=110) for _ in range(world))
+    res = {}
+    for _ in range(world):
+        r, lat, blk = q.get(timeout=110)
+        res[r] = (lat, blk)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert torch.equal(res[0], res[1])
-    # the whole batch in one process: rank r's prompts are rows [r*B, (r+1)*B)
-    parts = [_inputs(r, B) for r in range(world)]
-    ids, tm, spk, sm = (torch.cat([p[i] for p in parts]) for i in range(4))
-    full = _sample(_model(), ids, tm, spk, sm, _noise(world)).cpu()
-    assert torch.isfinite(full).all()
-    assert torch.equal(res[0], full), float((res[0] - full).abs().max())
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    from echo_tts_amd.inference import sample_euler_cfg_independent_guidances
+    from echo_tts_amd.inference_blockwise import sample_blockwise_euler_cfg_independent_guidances
+    m = _model()
+    ids, tm, spk, sm = _inputs()
+    full = sample_euler_cfg_independent_guidances(m, spk, sm, ids, tm, 11, sequence_length=N, **KW).cpu()
+    full_blk = sample_blockwise_euler_cfg_independent_guidances(m, spk, sm, ids, tm, 12, BLOCKS, **KW_BLK).cpu()
+    assert torch.isfinite(full).all() and torch.isfinite(full_blk).all()
+    assert torch.equal(res[0][0], full), float((res[0][0] - full).abs().max())
+    assert torch.equal(res[0][1], full_blk), float((res[0][1] - full_blk).abs().max())
