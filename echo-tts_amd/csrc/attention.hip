@@ -189,9 +189,17 @@ struct SegInfo {
 // item's gated output is stored after the NEXT item's Q loads and first K/V DMA have been issued, and
 // only those are waited for (vmcnt counts loads, LDS-DMA and stores in issue order), so the store
 // tail of one item overlaps the prologue of the next instead of a workgroup teardown + relaunch.
-template <int ABL, int NW, int ST, int KTT = 64, int PS = 0>
-__global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1) attn_bf16_kernel(EchoAttnArgs a_arg) {
+//
+// SP = 1: split-KV form for launches with fewer items than CUs (B = 1 sampler steps, blockwise
+// blocks). Item = (q block, split, row, head); split s of nsp walks tiles [s*n/nsp, (s+1)*n/nsp) of
+// the item's flat tile list and stores its UNNORMALISED partial (O fp32, m in exp2 units, l) to
+// `ws` (layout: attn_split_ws_bytes); attn_combine_kernel merges the splits, normalises, gates and
+// stores. Same tile math; only the summation order over keys differs from SP = 0 (fp32-close).
+template <int ABL, int NW, int ST, int KTT = 64, int PS = 0, int SP = 0>
+__global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
+    attn_bf16_kernel(EchoAttnArgs a_arg, float* ws, int nsp) {
   static_assert(!PS || (ABL == 0 && ST == 2), "persistent form: production schedule only");
+  static_assert(!SP || (ABL == 0 && ST == 2 && !PS), "split-KV form: production schedule only");
   constexpr int QB = 32 * NW;
   constexpr int DPT = KTT / (4 * NW);  // DMA wave-instructions per wave per K (or V) tile
   const uint64_t ts0 = (ABL & 128) ? rt_now() : 0;
@@ -208,6 +216,8 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1) at
   (void)a_arg;
   const int nqb = (kargs->n_q + QB - 1) / QB;
   const int nitems = PS ? nqb * kargs->rows * kargs->heads : (int)blockIdx.x + 1;
+  (void)ws;
+  (void)nsp;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h2 = lane >> 5, ql = lane & 31;
@@ -224,8 +234,10 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1) at
   // rows fastest: each XCD's contiguous block range then covers every row type (cond /
   // uncond-text / uncond-speaker rows have different key counts), and the CFG rows that share
   // one text/speaker K/V copy land on the same XCD
-  const int row = (L / nqb) % a.rows;
-  const int head = L / (nqb * a.rows);
+  const int Lr = SP ? L / (nqb * nsp) : L / nqb;
+  const int sp = SP ? (L / nqb) % nsp : 0;
+  const int row = Lr % a.rows;
+  const int head = Lr / a.rows;
   const int q0 = qb * QB;
   const int qi = q0 + w * 32 + ql;
   const int qc = min(qi, a.n_q - 1);
@@ -248,6 +260,12 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1) at
   ECHO_CURSOR_ADVANCE()
   Cursor dmc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // DMA / load side
   Cursor cpc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // compute side
+  if constexpr (SP) {
+    // this split's tile range of the flat list (scalar cursor walk; <= ~20 tiles)
+    const int tb = sp * ntiles / nsp, te = (sp + 1) * ntiles / nsp;
+    for (int i = 0; i < tb; ++i) { advance(dmc); advance(cpc); }
+    ntiles = te - tb;
+  }
 
   // DMA of the next tile (dmc) into buffer `buf`: 64 rows x 256 B for K and V = 32
   // wave-instructions of 1 KiB (4 rows each); lane-linear LDS image, XOR swizzle applied on the
@@ -520,7 +538,27 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1) at
     bf16_t* op = (bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qc * a.o_ld_tok + head * 128;
     const bf16_t* gp = a.gate ? (const bf16_t*)a.gate + row * a.g_ld_batch + (int64_t)qc * a.g_ld_tok + head * 128
                               : nullptr;
-    if constexpr (PS) {
+    if constexpr (SP) {
+      // partial O at chunk c = d / 4 (32 chunks of 4 floats), laid out [chunk][query] so the 32
+      // lanes of a half-wave store 512 contiguous bytes per instruction
+      if (valid) {
+        const int64_t it = ((int64_t)sp * a.rows + row) * a.heads + head;
+        float* wo = ws + it * 128 * a.n_q;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int rg = 0; rg < 4; ++rg) {
+            const int c = dt * 8 + 2 * rg + h2;
+            *(float4*)(wo + ((int64_t)c * a.n_q + qi) * 4) =
+                make_float4(o[dt][4 * rg], o[dt][4 * rg + 1], o[dt][4 * rg + 2], o[dt][4 * rg + 3]);
+          }
+        if (h2 == 0) {
+          float* wml = ws + (int64_t)nsp * a.rows * a.heads * 128 * a.n_q + (it * a.n_q + qi) * 2;
+          *(float2*)wml = make_float2(m_run == -INFINITY ? -INFINITY : m_run * sl2, lt);
+        }
+      }
+      (void)inv;
+    } else if constexpr (PS) {
       attn_pack_out(o, inv, h2, valid, gp, pend);
       pend_op = op;
       pend_valid = valid;
@@ -784,6 +822,52 @@ __global__ void __launch_bounds__(256, 2) attn_pipe_kernel(EchoAttnArgs a) {
     }
 }
 
+// ----------------------------------------------------------------------------- split-KV combine
+// One thread per (query, 8 output columns): M = max_s m_s, w_s = 2^(m_s - M),
+// out = round(round(sum_s w_s O_s / sum_s w_s l_s) * round(sigmoid(gate))) — the roundings of
+// attn_pack_out. 16 queries x 16 column groups per 256-thread block (query fastest: the partial
+// reads are 256-B runs, the 16-B output stores fill whole rows across the block).
+__global__ void __launch_bounds__(256) attn_combine_kernel(EchoAttnArgs a, const float* __restrict__ ws, int nsp) {
+  const int nqb = (a.n_q + 15) / 16;
+  const int qb = blockIdx.x % nqb, rh = blockIdx.x / nqb;  // rh = row * heads + head
+  const int row = rh / a.heads, head = rh % a.heads;
+  const int qi = qb * 16 + (threadIdx.x & 15), c8 = threadIdx.x >> 4;
+  if (qi >= a.n_q) return;
+  const int64_t per_split = (int64_t)a.rows * a.heads * 128 * a.n_q;
+  const float* ml = ws + nsp * per_split;
+  float mx = -INFINITY;
+  for (int s = 0; s < nsp; ++s) mx = fmaxf(mx, ml[(((int64_t)s * a.rows * a.heads + rh) * a.n_q + qi) * 2]);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, l = 0.f;
+  for (int s = 0; s < nsp; ++s) {
+    const int64_t it = (int64_t)s * a.rows * a.heads + rh;
+    const float2 m_l = *(const float2*)(ml + (it * a.n_q + qi) * 2);
+    if (m_l.x == -INFINITY) continue;  // split without a visible key for this query
+    const float wgt = __builtin_amdgcn_exp2f(m_l.x - mx);
+    const float* wo = ws + it * 128 * a.n_q;
+    const float4 lo = *(const float4*)(wo + ((int64_t)(2 * c8) * a.n_q + qi) * 4);
+    const float4 hi = *(const float4*)(wo + ((int64_t)(2 * c8 + 1) * a.n_q + qi) * 4);
+    acc[0] += wgt * lo.x; acc[1] += wgt * lo.y; acc[2] += wgt * lo.z; acc[3] += wgt * lo.w;
+    acc[4] += wgt * hi.x; acc[5] += wgt * hi.y; acc[6] += wgt * hi.z; acc[7] += wgt * hi.w;
+    l += wgt * m_l.y;
+  }
+  const float inv = 1.0f / l;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = rbf(acc[e] * inv);
+  if (a.gate) {
+    const uint4 g4 = *(const uint4*)((const bf16_t*)a.gate + row * a.g_ld_batch + (int64_t)qi * a.g_ld_tok + head * 128 +
+                                     8 * c8);
+    const uint32_t gg[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[2 * e] = rbf(v[2 * e] * rbf(sigmoid_f(bf2f(gg[e] & 0xffffu))));
+      v[2 * e + 1] = rbf(v[2 * e + 1] * rbf(sigmoid_f(bf2f(gg[e] >> 16))));
+    }
+  }
+  *(uint4*)((bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qi * a.o_ld_tok + head * 128 + 8 * c8) =
+      make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+}
+
 // ----------------------------------------------------------------------------- fp32 (parity mode)
 constexpr int FQ = 64, FKT = 32;
 
@@ -895,7 +979,8 @@ int attn_ps_grid(int nitems) {
 int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) {
   const int qb = (cfg == 1 || cfg == 2 || cfg == 4) ? 256 : 128;
   const dim3 grid(attn_grid(a, qb));
-#define ECHO_ATTN_LAUNCH(A, NW, ST, ...) hipLaunchKernelGGL((attn_bf16_kernel<A, NW, ST, ##__VA_ARGS__>), grid, dim3(64 * NW), 0, s, *a)
+#define ECHO_ATTN_LAUNCH(A, NW, ST, ...) \
+  hipLaunchKernelGGL((attn_bf16_kernel<A, NW, ST, ##__VA_ARGS__>), grid, dim3(64 * NW), 0, s, *a, (float*)nullptr, 1)
 #define ECHO_ATTN_ABLS(NW, ST)                        \
   switch (abl) {                                      \
     case 0: ECHO_ATTN_LAUNCH(0, NW, ST); break;       \
@@ -932,13 +1017,13 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       if (abl) return ECHO_EINVAL;
       const int ps_grid = attn_ps_grid(grid.x);
       if (ps_grid <= 0) return ECHO_EINVAL;
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a);
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a, (float*)nullptr, 1);
       break;
     }
     case 6: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 2, 32); break;
     case 9:  // 2 waves x 32 queries per workgroup (production for launches that cannot fill the CUs)
       if (abl) return ECHO_EINVAL;
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 2, 2>), dim3(attn_grid(a, 64)), dim3(128), 0, s, *a);
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 2, 2>), dim3(attn_grid(a, 64)), dim3(128), 0, s, *a, (float*)nullptr, 1);
       break;
     case 7: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 3, 32); break;
     default: return ECHO_EINVAL;
@@ -967,12 +1052,78 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
     // R = 3: 43.2 -> 54.1 us, R = 1: 38.7 -> 47.1 us: the per-workgroup tile chain stays as long and
     // each wave issues twice the DMA; that case needs split-KV chains)
     if (nitems > ps_grid && nitems <= 3 * ps_grid)
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a);
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a, (float*)nullptr, 1);
     else
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(nitems), dim3(256), 0, s, *a);
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(nitems), dim3(256), 0, s, *a, (float*)nullptr, 1);
   } else {
     hipLaunchKernelGGL(attn_f32_kernel, dim3(attn_grid(a, FQ)), dim3(64), 0, s, *a);
   }
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+namespace {
+int g_attn_split_override = -1;  // echo_attention_set_split: force nsplit (diagnostics), -1 = policy
+
+int cu_count() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      return 256;
+    cus = n;
+  }
+  return cus;
+}
+}  // namespace
+
+extern "C" int64_t echo_attention_split_ws_bytes(const EchoAttnArgs* a, int32_t nsplit) {
+  if (!a || nsplit < 2 || a->rows <= 0 || a->heads <= 0 || a->n_q <= 0) return 0;
+  return (int64_t)nsplit * a->rows * a->heads * a->n_q * (128 + 2) * (int64_t)sizeof(float);
+}
+
+extern "C" int32_t echo_attention_pick_split(const EchoAttnArgs* a) {
+  if (check_attn_args(a) || a->dtype != ECHO_BF16) return 1;
+  int tiles = 0;  // upper bound of an item's flat tile list (capacities; lens are on the device)
+  for (int s = 0; s < a->nseg; ++s)
+    if (a->seg[s].k) tiles += (a->seg[s].capacity + KT - 1) / KT;
+  int nsp;
+  if (g_attn_split_override >= 0) {
+    nsp = g_attn_split_override;
+  } else {
+    // measured (tools/bench_attn.py --splits, MI355X, 256 CUs; us for split counts 1 / 2 / 3 / 4):
+    //   640 queries, R = 3 (240 items): 38.5 / 44.0 / 50.1 / 52.7  -> never
+    //   640 queries, R = 1 ( 80 items): 35.7 / 30.0 / 29.7 / 31.8  -> 3
+    //   160 queries, R = 3 ( 96 items): 28.7 / 25.1 / 26.5 / 27.1  -> 2
+    //   160 queries, R = 1 ( 32 items): 27.9 / 21.7 / 21.0 / 21.0  -> 3-4
+    // the per-workgroup prologue (Q + first K/V tile) and the partials' round trip through L2/HBM
+    // (nsplit x the output in fp32) bound the gain: split only launches that leave half the CUs idle
+    const int nitems = attn_grid(a, 128), cus = cu_count();
+    nsp = nitems * 2 > cus ? 1 : nitems * 8 >= cus * 3 ? 2 : nitems * 8 > cus ? 3 : 4;
+    nsp = min(nsp, tiles / 3);
+  }
+  return max(1, min(nsp, min(tiles, 16)));
+}
+
+extern "C" int echo_attention_set_split(int32_t nsplit) {
+  if (nsplit < -1 || nsplit > 16) return ECHO_EINVAL;
+  g_attn_split_override = nsplit;
+  return 0;
+}
+
+extern "C" int echo_attention_split(const EchoAttnArgs* a, int32_t nsplit, void* ws, int64_t ws_bytes, void* stream) {
+  const int rc = check_attn_args(a);
+  if (rc) return rc;
+  if (nsplit <= 1) return echo_attention(a, stream);
+  if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
+  if (nsplit > 16) return ECHO_EINVAL;
+  if (!ws || (uintptr_t)ws % 16 || ws_bytes < echo_attention_split_ws_bytes(a, nsplit)) return ECHO_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 0, 1>), dim3(attn_grid(a, 128) * nsplit), dim3(256), 0, s, *a,
+                     (float*)ws, (int)nsplit);
+  ECHO_LAUNCH_CHECK();
+  hipLaunchKernelGGL(attn_combine_kernel, dim3(a->rows * a->heads * ((a->n_q + 15) / 16)), dim3(256), 0, s, *a,
+                     (const float*)ws, (int)nsplit);
   ECHO_LAUNCH_CHECK();
   return 0;
 }

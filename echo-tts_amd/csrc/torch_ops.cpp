@@ -301,7 +301,16 @@ void joint_attention_out(const Tensor& q, const optional<Tensor>& gate, at::Tens
                          at::IntArrayRef seg_causal, const Tensor& out, double scale) {
   EchoAttnArgs a = attn_args(q, gate, seg_k, seg_v, seg_len, seg_batch_mod, seg_causal, out, scale);
   c10::DeviceGuard guard(q.device());
-  check_rc(echo_attention(&a, stream_of(q)), "echo_hip.joint_attention");
+  // launches that would leave most CUs idle run the split-KV form; its workspace comes from the
+  // caching allocator (graph-private pool under hipGraph capture)
+  const int32_t nsp = echo_attention_pick_split(&a);
+  if (nsp > 1) {
+    const int64_t bytes = echo_attention_split_ws_bytes(&a, nsp);
+    Tensor ws = at::empty({(bytes + 3) / 4}, q.options().dtype(at::kFloat));
+    check_rc(echo_attention_split(&a, nsp, ws.data_ptr(), bytes, stream_of(q)), "echo_hip.joint_attention");
+  } else {
+    check_rc(echo_attention(&a, stream_of(q)), "echo_hip.joint_attention");
+  }
 }
 
 Tensor joint_attention(const Tensor& q, const optional<Tensor>& gate, at::TensorList seg_k, at::TensorList seg_v,

@@ -11,6 +11,7 @@ PyTorch only provides device memory and the stream; every arithmetic op runs in
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 import sys
@@ -131,6 +132,19 @@ def attention(q: Tensor, segments: Sequence[Segment], out: Optional[Tensor] = No
         return T().joint_attention(q, gate, ks, vs, lens, bms, causal, scale)
     T().joint_attention_out(q, gate, ks, vs, lens, bms, causal, out, scale)
     return out
+
+
+@contextlib.contextmanager
+def attention_split(nsplit: int):
+    """Force the split-KV count of `attention` inside the block (1 = never split; tests and
+    tools/bench_attn.py). Outside it the host policy (echo_attention_pick_split) decides."""
+    rc = lib().echo_attention_set_split(int(nsplit))
+    if rc:
+        raise RuntimeError(f"echo_attention_set_split({nsplit}) failed: {rc}")
+    try:
+        yield
+    finally:
+        lib().echo_attention_set_split(-1)
 
 
 def attention_variant(q: Tensor, segments: Sequence[Segment], out: Tensor, gate: Optional[Tensor] = None,

@@ -118,6 +118,20 @@ typedef struct {
  * JointAttention.forward (model.py:237-264) and SelfAttention.forward (model.py:144-157). */
 int echo_attention(const EchoAttnArgs* args, void* stream);
 
+/* Split-KV form of echo_attention for launches that leave most CUs idle (B = 1 sampler steps,
+ * blockwise blocks): each (128-query block, row, head) item's key tiles are split over `nsplit`
+ * workgroups that store unnormalised partials (O fp32, running max, row sum) into `ws`, and a
+ * combine pass merges them, normalises, gates and stores `out` (same roundings as echo_attention;
+ * only the fp32 summation order over keys differs). nsplit <= 1 runs echo_attention.
+ * `ws`: device, 16-B aligned, >= echo_attention_split_ws_bytes(args, nsplit) bytes.
+ * Replaces the same reference lines as echo_attention (model.py:237-264, 144-157). */
+int echo_attention_split(const EchoAttnArgs* args, int32_t nsplit, void* ws, int64_t ws_bytes, void* stream);
+int64_t echo_attention_split_ws_bytes(const EchoAttnArgs* args, int32_t nsplit);
+/* Host policy: the split count echo_attention_split should use for these shapes (1 = none). */
+int32_t echo_attention_pick_split(const EchoAttnArgs* args);
+/* Diagnostics: force the policy's answer (0/1 = never split, 2..16), -1 = back to the policy. */
+int echo_attention_set_split(int32_t nsplit);
+
 /* Diagnostics only (tools/bench_attn.py, tools/attn_timeline.py; never on the sampling path):
  * measurement variants of the bf16 attention kernel. variant 0 = the production kernel;
  * ablation != 0 removes parts of the work (results are then WRONG, timing only); ablation bit 128

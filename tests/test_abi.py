@@ -156,3 +156,35 @@ def test_torch_ops_fake_kernels():
         assert T.cast_from_f32(x, bf).dtype == bf
         assert T.timestep_embedding(torch.empty(40, device="cuda"), torch.empty(256, device="cuda"), bf).shape == (40, 512)
         assert T.silu(a).shape == a.shape
+
+
+def test_attention_split_host_policy(lib):
+    """Split-KV policy (attention.hip echo_attention_pick_split, host-only): the sampler's B = 1
+    decoder launches (R = 1 / 3 rows of 640 queries) split their keys, the B = 16 ones (R = 16 / 48)
+    do not; the override knob and the workspace size (nsplit x rows x heads x n_q x 130 floats)."""
+    import ctypes as C
+    from echo_tts_amd import _lib as L
+    fake = 1 << 20  # never dereferenced by the host policy
+
+    def args(R, B, n_q=640):
+        a = L.AttnArgs()
+        a.dtype, a.rows, a.n_q, a.heads, a.nseg, a.scale = 0, R, n_q, 16, 3, 128 ** -0.5  # ECHO_BF16
+        a.q = a.out = a.gate = fake
+        a.q_ld_tok = a.o_ld_tok = a.g_ld_tok = 4 * 16 * 128
+        a.q_ld_batch = a.o_ld_batch = a.g_ld_batch = n_q * 4 * 16 * 128
+        for i, (cap, bm) in enumerate(((n_q, R), (448, B), (160, B))):
+            s = a.seg[i]
+            s.k = s.v = fake
+            s.ld_tok, s.ld_batch, s.batch_mod, s.capacity = 2 * 16 * 128, cap * 2 * 16 * 128, bm, cap
+        return a
+
+    assert lib.echo_attention_split_ws_bytes(C.byref(args(1, 1)), 3) == 3 * 1 * 16 * 640 * 130 * 4
+    picks = {R: lib.echo_attention_pick_split(C.byref(args(R, B))) for R, B in ((1, 1), (3, 1), (16, 16), (48, 16))}
+    assert picks[1] == 3 and picks[3] == 1 and picks[16] == 1 and picks[48] == 1, picks
+    assert lib.echo_attention_pick_split(C.byref(args(3, 1, n_q=160))) == 2  # a blockwise block, CFG rows
+    assert lib.echo_attention_set_split(5) == 0
+    try:
+        assert lib.echo_attention_pick_split(C.byref(args(48, 16))) == 5
+    finally:
+        assert lib.echo_attention_set_split(-1) == 0
+    assert lib.echo_attention_set_split(17) != 0

@@ -305,7 +305,8 @@ def test_attention_variants_match_production(variant):
     tl = torch.tensor([50, 71, 0, 0, 50, 71], dtype=torch.int32, device=DEV)
     segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2]), ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=B)]
     ref = torch.empty(R, N, H, 128, device=DEV, dtype=BF)
-    ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
+    with ops.attention_split(1):  # the unsplit production kernel (this small launch would split)
+        ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
     got = torch.empty_like(ref)
     ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=variant)
     if variant in (0, 8, 9):
@@ -321,30 +322,87 @@ def test_attention_variants_match_production(variant):
         assert (st[:n, 3] >= st[:n, 0]).all() and (st[:n, 0] > 0).all()
 
 
+def _small_batch_segments(B, R, n_q, H=16, T=448, P=160, tl_valid=300, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    qkvg = torch.randn(R, n_q, 4, H, 128, device=DEV, generator=g).to(BF)
+    kt = torch.randn(B, T, 2, H, 128, device=DEV, generator=g).to(BF)
+    ks = torch.randn(B, P, 2, H, 128, device=DEV, generator=g).to(BF)
+    tl = torch.tensor(([tl_valid] * B + [0] * B + [tl_valid] * B)[:R], dtype=torch.int32, device=DEV)
+    sl = torch.tensor(([P] * 2 * B + [0] * B)[:R], dtype=torch.int32, device=DEV)
+    segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2]),
+            ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=B),
+            ops.Segment(ks[:, :, 0], ks[:, :, 1], lens=sl, batch_mod=B)]
+    return qkvg, segs
+
+
+def split_close(got, ref, r64):
+    """Split-KV vs the unsplit kernel and an fp64 reference. The roundings are the same, but each split
+    forms its bf16 P against its own running max and the fp32 sums run in another order, so the two
+    kernels differ by about (bf16 P rounding) / sqrt(keys) of the output scale (random signs), one
+    bf16 ulp on a fraction of the elements. Gate: no further from fp64 than the unsplit kernel, in
+    rel-L2 and in the largest element error."""
+    o, r, t = got.float().cpu(), ref.float().cpu(), r64.float().cpu()
+    assert torch.isfinite(o).all()
+    assert rel(o, r) < 4e-3, rel(o, r)
+    e_split, e_ref = rel(o, t), rel(r, t)
+    assert e_split <= 1.25 * e_ref + 1e-4, (e_split, e_ref)
+    m_split, m_ref = float((o - t).abs().max()), float((r - t).abs().max())
+    assert m_split <= 2.0 * m_ref + 1e-4, (m_split, m_ref)  # one more bf16 ulp at the worst element
+    return float((o != r).double().mean())
+
+
 @pytest.mark.parametrize("B", [1, 3])
 @pytest.mark.parametrize("n_q", [640, 600, 200])
 def test_attention_small_batch_two_wave(B, n_q):
     """B = 1 sampling (3 CFG rows, then 1 row) cannot fill the CUs with 128-query workgroups: the
-    production path and the 64-query-workgroup variant 9 are bitwise equal to variant 0 there."""
-    H, T, P = 16, 448, 160
+    64-query-workgroup variant 9 and the unsplit production kernel are bitwise equal to variant 0
+    there; the production path (split-KV by the host policy) is split-close to it."""
     for R in (3 * B, B):
-        qkvg = torch.randn(R, n_q, 4, H, 128, device=DEV).to(BF)
-        kt = torch.randn(B, T, 2, H, 128, device=DEV).to(BF)
-        ks = torch.randn(B, P, 2, H, 128, device=DEV).to(BF)
-        tl = torch.tensor(([300] * B + [0] * B + [300] * B)[:R], dtype=torch.int32, device=DEV)
-        sl = torch.tensor(([P] * 2 * B + [0] * B)[:R], dtype=torch.int32, device=DEV)
-        segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2]),
-                ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=B),
-                ops.Segment(ks[:, :, 0], ks[:, :, 1], lens=sl, batch_mod=B)]
-        got = torch.full((R, n_q, H, 128), float("nan"), device=DEV, dtype=BF)
+        qkvg, segs = _small_batch_segments(B, R, n_q)
+        got = torch.full((R, n_q, 16, 128), float("nan"), device=DEV, dtype=BF)
         ref = torch.empty_like(got)
-        ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
         ops.attention_variant(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3], variant=0)
+        with ops.attention_split(1):
+            ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
         torch.cuda.synchronize()
         assert torch.equal(got, ref)
         got.fill_(float("nan"))
         ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=9)
         assert torch.equal(got, ref)
+        got.fill_(float("nan"))
+        ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
+        split_close(got, ref, ref_attention(qkvg[:, :, 0], segs, qkvg[:, :, 3], 128 ** -0.5, BF))
+
+
+@pytest.mark.parametrize("nsplit", [2, 3, 5, 8, 16])
+@pytest.mark.parametrize("R,n_q", [(1, 640), (3, 640), (3, 160), (1, 37)])
+def test_attention_split_kv(nsplit, R, n_q):
+    """Split-KV form (echo_attention_split): every forced split count, incl. more splits than an
+    item has tiles (empty splits store m = -inf and drop out of the combine) and rows whose text /
+    speaker segments are empty; against the unsplit kernel (split_close) and an fp64 reference."""
+    qkvg, segs = _small_batch_segments(1, R, n_q, H=4, tl_valid=271)
+    ref = torch.empty(R, n_q, 4, 128, device=DEV, dtype=BF)
+    with ops.attention_split(1):
+        ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
+    got = torch.full_like(ref, float("nan"))
+    with ops.attention_split(nsplit):
+        ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
+        ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])  # workspace reuse
+    torch.cuda.synchronize()
+    split_close(got, ref, ref_attention(qkvg[:, :, 0], segs, qkvg[:, :, 3], 128 ** -0.5, BF))
+
+
+@pytest.mark.parametrize("L_", [37, 160, 333])
+def test_attention_split_kv_causal(L_):
+    """Split-KV on a causal (encoder) segment: queries whose split holds no visible key."""
+    B, H = 1, 3
+    qkv = torch.randn(B, L_, 4, H, 128, device=DEV).to(BF)
+    segs = [ops.Segment(qkv[:, :, 1], qkv[:, :, 2], causal=True)]
+    out = torch.empty(B, L_, H, 128, device=DEV, dtype=BF)
+    with ops.attention_split(4):
+        ops.attention(qkv[:, :, 0], segs, out=out, gate=None)
+    ref = ref_attention(qkv[:, :, 0], segs, None, 128 ** -0.5, BF)
+    assert rel(out, ref) < 6e-3
 
 
 @pytest.mark.parametrize("n_q,cfg", [(640, True), (600, True), (640, False), (600, False)])

@@ -34,9 +34,13 @@ def main():
     ap.add_argument("--stamps", default=None, help="ablation 128: write the last call's timeline (.npy)")
     ap.add_argument("--batch", type=int, default=16, help="prompts B (rows 3B with CFG, B without)")
     ap.add_argument("--compare", default=None, help="two variant ids 'A,B': interleaved rounds + bitwise check")
+    ap.add_argument("--nq", type=int, default=640, help="queries per row (160 = a blockwise block)")
+    ap.add_argument("--splits", default=None,
+                    help="comma list of forced split-KV counts (1 = unsplit) for the production op: interleaved "
+                         "rounds, median per count")
     args = ap.parse_args()
     dev = "cuda"
-    B, N, H, T, P = args.batch, 640, 16, 448, 160
+    B, N, H, T, P = args.batch, args.nq, 16, 448, 160
     for R, tl_c, sl_c in ((3 * B, [388] * B + [0] * B + [388] * B, [160] * 2 * B + [0] * B),
                           (B, [388] * B, [160] * B)):
         if args.rows and R != args.rows:
@@ -68,6 +72,19 @@ def main():
                 ma, mb = sorted(ta)[2], sorted(tb)[2]
                 print(f"R={R:3d} {name:10s} v{va} {ma * 1e3:8.1f} us  v{vb} {mb * 1e3:8.1f} us  "
                       f"bitwise_equal={same}", flush=True)
+                continue
+            if args.splits:
+                counts = [int(v) for v in args.splits.split(",")]
+                f = lambda: ops.attention(qkvg[:, :, 0], segs, out=out, gate=qkvg[:, :, 3])  # noqa: E731
+                tm = {c: [] for c in counts}
+                for _ in range(7):
+                    for c in counts:
+                        with ops.attention_split(c):
+                            f()
+                            tm[c].append(timeit(f, rounds=1))
+                pol = ops.lib().echo_attention_set_split(-1)
+                line = "  ".join(f"s{c} {sorted(v)[3] * 1e3:7.1f}" for c, v in tm.items())
+                print(f"R={R:3d} {name:10s} us by split: {line}", flush=True)
                 continue
             if args.variant is None and not args.ablation:
                 fn = lambda: ops.attention(qkvg[:, :, 0], segs, out=out, gate=qkvg[:, :, 3])  # noqa: E731
