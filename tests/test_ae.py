@@ -210,11 +210,51 @@ def _code_report(codes, ref):
     return float(eq.float().mean()), float(eq.all(dim=1).float().mean())
 
 
+def rvq_flip_gaps(z, W, codes, n_codebooks=9):
+    """Where do OUR RVQ codes differ from the oracle's argmin, and by how much? The oracle's RVQ
+    (ae_oracle.rvq_codes, autoencoder.py:184-221 / 145-157) is re-run on `z` (our pre_module output)
+    teacher-forced with OUR codes, so every stage sees the input our kernel saw (up to fp32
+    rounding of the stage's in_proj); at each decision the distances |e|^2 - 2e.c + |c|^2 to all
+    normalised codebook entries are formed in fp64. Returns (gaps, margins): for every decision
+    where our code differs from the fp64 argmin, d64[ours] - d64[argmin] (0 = exact tie); and for
+    every decision, the fp64 gap between the best and second-best entries (the typical margin)."""
+    import torch.nn.functional as F
+    gaps, margins = [], []
+    residual = z.double()
+    stacks = [("quantizer.semantic_quantizer", 1), ("quantizer.quantizer", n_codebooks)]
+    col = 0
+    for name, nq in stacks:
+        z_q = 0
+        r = residual
+        for q in range(nq):
+            p = f"{name}.quantizers.{q}"
+            z_e = F.conv1d(r, W[f"{p}.in_proj.weight"].double(), W[f"{p}.in_proj.bias"].double())
+            enc = F.normalize(z_e.transpose(1, 2).reshape(-1, z_e.shape[1]))
+            cb = F.normalize(W[f"{p}.codebook.weight"].double())
+            dist = enc.pow(2).sum(1, keepdim=True) - 2 * enc @ cb.t() + cb.pow(2).sum(1, keepdim=True).t()
+            ours = codes[:, col].reshape(-1)
+            best = dist.min(1)
+            two = dist.topk(2, dim=1, largest=False).values
+            margins.append(two[:, 1] - two[:, 0])
+            d_ours = dist.gather(1, ours.view(-1, 1)).squeeze(1)
+            off = ours != best.indices
+            gaps.append(d_ours[off] - best.values[off])
+            zq = F.embedding(codes[:, col], W[f"{p}.codebook.weight"].double()).transpose(1, 2)
+            zq = F.conv1d(zq, W[f"{p}.out_proj.weight"].double(), W[f"{p}.out_proj.bias"].double())
+            z_q = z_q + zq
+            r = r - zq
+            col += 1
+        if name.endswith("semantic_quantizer"):
+            residual = residual - z_q
+    return torch.cat(gaps), torch.cat(margins)
+
+
 # fp32: stages within accumulation-order error of the reference; the codes are argmins over
-# 1024/4096 entries, so a stage error of ~1e-6 can flip a near-tie: require >= 97 % of frames
-# with all codes equal and latents (whose error is dominated by flipped frames) within 0.1 rel-L2.
-# Teacher-forced (the oracle's RVQ on OUR pre_module output) the codes must agree exactly on >= 99 %
-# of the decisions: that isolates the RVQ kernel from upstream rounding.
+# 1024/4096 entries, so a stage error of ~1e-6 could flip a near-tie. Teacher-forced (the oracle's
+# RVQ on OUR pre_module output) the codes must agree on >= 99 % of the decisions, and every
+# decision that departs from the fp64 argmin must be a certified near-tie (rvq_flip_gaps); >= 99 %
+# of frames must match the reference's codes, and the latents must then be within the stage
+# tolerance.
 @pytest.mark.gpu
 def test_hip_encode_matches_reference_fp32():
     g = load_golden("ae_enc_fp32")
@@ -233,7 +273,17 @@ def test_hip_encode_matches_reference_fp32():
           f"latents {lat_err:.2e}")
     for k, v in errs.items():
         assert v < 1e-4, (k, v)
-    assert tf_frac >= 0.99 and frames >= 0.97 and lat_err < 0.1
+    assert tf_frac >= 0.99 and frames >= 0.99
+    # every code where the kernel departs from the fp64 argmin is a near-tie: the two distances agree
+    # to within fp32 rounding of a distance between unit vectors (|d| <= 4; the kernel forms it in
+    # fp32 from an in_proj of 1024 fp32 products), far below the typical best/second-best margin
+    gaps, margins = rvq_flip_gaps(st["pre_module"].cpu(), enc_weights(torch.float32), codes)
+    print(f"RVQ: {gaps.numel()} of {margins.numel()} decisions off the fp64 argmin; max gap "
+          f"{float(gaps.max()) if gaps.numel() else 0.0:.2e}; median best/second margin {float(margins.median()):.2e}")
+    assert gaps.numel() == 0 or float(gaps.max()) <= 2e-6, float(gaps.max())
+    # measured on MI355X: 0 of 1600 decisions off the argmin, every frame equal, latents 3.3e-7: the
+    # latent gate is the stage tolerance unless a certified near-tie flipped a frame
+    assert lat_err < (1e-4 if gaps.numel() == 0 and frames == 1.0 else 0.1), lat_err
 
 
 @pytest.mark.gpu
@@ -279,7 +329,7 @@ def test_hip_speaker_latent_and_mask():
     assert torch.equal(mask.cpu(), g["speaker_mask"]) and lat.shape == g["speaker_latent"].shape
     err = rel_l2(lat.cpu(), g["speaker_latent"])
     print(f"speaker latents rel-L2 {err:.2e}")
-    assert err < 0.1
+    assert err < 1e-4  # measured 3.3e-7 (every RVQ code equal to the reference's, test above)
     # the batched pass equals per-chunk encodes of the same chunks
     one = ae.encoder.ae_encode(comps, mean, scale, g["audio"][:, :meta["chunk"]].unsqueeze(0).cuda())
     assert rel_l2(one.cpu(), lat[:, :one.shape[1]].cpu()) < 1e-5
