@@ -1450,9 +1450,15 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   if (!a || !a->A || !a->W || !a->C) return ECHO_EINVAL;
   if (a->M <= 0 || a->N <= 0 || a->K <= 0 || a->batch <= 0) return ECHO_ESHAPE;
   if (a->K % 64 || a->N % 16 || a->lda % 8 || a->ldw % 8 || a->ldc % 8) return ECHO_EALIGN;
+  if (a->dtype != ECHO_BF16 && a->dtype != ECHO_F32) return ECHO_EDTYPE;
   if (a->epilogue == ECHO_EPI_RESID && !a->aux) return ECHO_EINVAL;
   if (a->epilogue == ECHO_EPI_SWIGLU && (a->N % 32 || a->bias)) return ECHO_EINVAL;
   if (a->epilogue < 0 || a->epilogue > 4) return ECHO_EINVAL;
+  // leading dimensions cover the rows they address (conv mode: A rows are conv_c wide)
+  if (a->lda < (a->conv_taps > 0 ? a->conv_c : a->K) || a->ldw < a->K ||
+      a->ldc < (a->epilogue == ECHO_EPI_SWIGLU ? a->N / 2 : a->N) ||
+      (a->epilogue == ECHO_EPI_RESID && a->ld_aux < a->N))
+    return ECHO_ESHAPE;
   if (a->act < 0 || a->act > ECHO_ACT_SNAKE || (a->act == ECHO_ACT_SNAKE && !a->act_alpha)) return ECHO_EINVAL;
   if (a->conv_taps < 0 || (a->conv_taps > 0 && (a->conv_c <= 0 || a->conv_dil <= 0 ||
                                                  (int64_t)a->conv_taps * a->conv_c != a->K ||
