@@ -67,6 +67,14 @@ __device__ __forceinline__ T sel4(int sg, T a0, T a1, T a2, T a3) {
 // 32-63 columns 8k+8 .. 8k+15, so gate loads and output stores are 16 B per lane (8 + 8 instead of
 // 16 + 16 8-B accesses; the store tail is issue-bound). Same roundings as the reference
 // (model.py:255-264: SDPA out bf16, sigmoid(gate) bf16, product bf16).
+// sigmoid from the hardware v_exp_f32 / v_rcp_f32 (≈3 ulp fp32): rounded to bf16 it equals the rounded
+// precise fp32 sigmoid (expf + IEEE division) for every bf16 input except the three whose results are
+// fp32 denormals (x = -87.5, -88, -88.5: the hardware ops flush them to 0) — checked exhaustively over all
+// 65536 inputs on MI355X (tools/sigmoid_exhaustive.hip). Callers take the precise path for x < -87.
+__device__ __forceinline__ float sigmoid_hw(float v) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.44269504088896341f));
+}
+
 __device__ __forceinline__ void attn_pack_out(const f32x16 (&o)[4], float inv, int h2, bool valid, const bf16_t* gp,
                                               uint4 (&v4)[8]) {
   uint32_t w[16][2];
@@ -87,19 +95,37 @@ __device__ __forceinline__ void attn_pack_out(const f32x16 (&o)[4], float inv, i
   uint4 g4[8];
 #pragma unroll
   for (int pk = 0; pk < 8; ++pk) g4[pk] = *(const uint4*)(gp + 16 * pk + c0);
+  // out = round(round(o / l) * round(sigmoid(gate))) (model.py:255-264 roundings). The precise path is
+  // needed only for gates below -87 (bf16 bits above 0xC2AE as unsigned 16-bit: negative, magnitude
+  // > 87; NaNs also land there): one packed-u16 max over the lane's 64 gates decides.
+  typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
+  u16x2 gmax = {0, 0};
 #pragma unroll
   for (int pk = 0; pk < 8; ++pk) {
-    const uint32_t vv[4] = {v4[pk].x, v4[pk].y, v4[pk].z, v4[pk].w};
-    const uint32_t gg[4] = {g4[pk].x, g4[pk].y, g4[pk].z, g4[pk].w};
-    uint32_t r[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float a0 = rbf(bf2f(vv[e] & 0xffffu) * rbf(sigmoid_f(bf2f(gg[e] & 0xffffu))));
-      const float a1 = rbf(bf2f(vv[e] >> 16) * rbf(sigmoid_f(bf2f(gg[e] >> 16))));
-      r[e] = pack2bf(a0, a1);
-    }
-    v4[pk] = make_uint4(r[0], r[1], r[2], r[3]);
+    gmax = __builtin_elementwise_max(gmax, __builtin_bit_cast(u16x2, g4[pk].x));
+    gmax = __builtin_elementwise_max(gmax, __builtin_bit_cast(u16x2, g4[pk].y));
+    gmax = __builtin_elementwise_max(gmax, __builtin_bit_cast(u16x2, g4[pk].z));
+    gmax = __builtin_elementwise_max(gmax, __builtin_bit_cast(u16x2, g4[pk].w));
   }
+  const bool tiny = gmax[0] > 0xC2AEu || gmax[1] > 0xC2AEu;
+  auto gated = [&](bool precise) __attribute__((always_inline)) {
+#pragma unroll
+    for (int pk = 0; pk < 8; ++pk) {
+      const uint32_t vv[4] = {v4[pk].x, v4[pk].y, v4[pk].z, v4[pk].w};
+      const uint32_t gg[4] = {g4[pk].x, g4[pk].y, g4[pk].z, g4[pk].w};
+      uint32_t r[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float g0 = bf2f(gg[e] & 0xffffu), g1 = bf2f(gg[e] >> 16);
+        const float s0 = precise ? sigmoid_f(g0) : sigmoid_hw(g0);
+        const float s1 = precise ? sigmoid_f(g1) : sigmoid_hw(g1);
+        r[e] = pack2bf(rbf(bf2f(vv[e] & 0xffffu) * rbf(s0)), rbf(bf2f(vv[e] >> 16) * rbf(s1)));
+      }
+      v4[pk] = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+  };
+  if (__builtin_expect(__any(tiny), 0)) gated(true);
+  else gated(false);
 }
 
 // 8 16-B stores per valid lane (a wave with any valid lane issues exactly 8 store instructions)
@@ -860,8 +886,9 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(EchoAttnArgs a, const
     const uint32_t gg[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      v[2 * e] = rbf(v[2 * e] * rbf(sigmoid_f(bf2f(gg[e] & 0xffffu))));
-      v[2 * e + 1] = rbf(v[2 * e + 1] * rbf(sigmoid_f(bf2f(gg[e] >> 16))));
+      const float g0 = bf2f(gg[e] & 0xffffu), g1 = bf2f(gg[e] >> 16);  // sigmoid_hw: see attn_pack_out
+      v[2 * e] = rbf(v[2 * e] * rbf(g0 < -87.0f ? sigmoid_f(g0) : sigmoid_hw(g0)));
+      v[2 * e + 1] = rbf(v[2 * e + 1] * rbf(g1 < -87.0f ? sigmoid_f(g1) : sigmoid_hw(g1)));
     }
   }
   *(uint4*)((bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qi * a.o_ld_tok + head * 128 + 8 * c8) =

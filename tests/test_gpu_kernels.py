@@ -518,6 +518,34 @@ def test_attention_causal(dtype, L_):
     assert rel(out, ref) < (6e-3 if dtype == BF else 1e-5)
 
 
+@pytest.mark.parametrize("split", [1, 3])
+def test_attention_gate_extremes(split):
+    """The gate's sigmoid comes from the hardware exp/rcp, which rounds to the same bf16 as the precise
+    fp32 sigmoid for every bf16 input except x in {-87.5, -88, -88.5} (denormal results, flushed by the
+    hardware; tools/sigmoid_exhaustive.hip): gates below -87 take the precise path, so those outputs
+    are the reference's tiny non-zero values, not 0 (unsplit kernel and the split-KV combine)."""
+    B, N, H = 1, 96, 2
+    g = torch.Generator().manual_seed(5)
+    qkvg = torch.randn(B, N, 4, H, 128, generator=g)
+    special = torch.tensor([-87.5, -88.0, -88.5, -87.0, -100.0, -200.0, 87.5, 0.0])
+    qkvg[:, :, 3, :, :8] = special
+    qkvg = qkvg.to(BF).to(DEV)
+    segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2])]
+    out = torch.empty(B, N, H, 128, device=DEV, dtype=BF)
+    with ops.attention_split(split):
+        ops.attention(qkvg[:, :, 0], segs, out=out, gate=qkvg[:, :, 3])
+    ref = ref_attention(qkvg[:, :, 0], segs, qkvg[:, :, 3], 128 ** -0.5, BF)
+    o, r = out.float().cpu()[..., :8], ref[..., :8]
+    assert torch.equal(o[..., 4:] == 0, r[..., 4:] == 0)          # -100, -200 -> 0; 87.5, 0 -> not 0
+    # the denormal sigmoids survive: the outputs are bf16 denormals (a few significant bits; some
+    # products underflow to 0 in the reference too) — equal to the reference's where both attention
+    # outputs round alike; with a flushed sigmoid every one of them would be 0
+    nz_o, nz_r = int((o[..., :3] != 0).sum()), int((r[..., :3] != 0).sum())
+    assert nz_r > 0 and nz_o >= 0.9 * nz_r, (nz_o, nz_r)
+    assert float((o[..., :3] == r[..., :3]).double().mean()) > 0.8
+    assert rel(out, ref) < 6e-3
+
+
 def test_attention_key_padding_spike():
     """A large score in the last valid key forces the online-softmax rescale branch."""
     B, N, H = 1, 130, 1
