@@ -2,7 +2,10 @@
 
 Public names and signatures are the reference's:
   tokenizer_encode (:152-182), get_text_input_ids_and_mask (:185-217),
-  ae_encode / ae_decode (:223-235), get_speaker_latent_and_mask (:250-309),
+  ae_encode / ae_decode / ae_reconstruct (:223-247), get_speaker_latent_and_mask (:250-309),
+  PCAState + load_pca_state (local form of load_pca_state_from_hf, :116-137),
+  load_model / load_fish_ae (local forms of load_model_from_hf / load_fish_ae_from_hf, :14-105;
+  no download: the same safetensors files from a path), compile_fish_ae (:108-113),
   find_flattening_point / crop_audio_to_flattening_point (:315-338),
   compile_model (:72-77), SampleFn (:341-343), sample_pipeline (:346-400), KVCache (:406),
   _concat_kv_caches (:409-417), _multiply_kv_cache (:420-428),
@@ -37,6 +40,41 @@ class PCAState:
     pca_components: torch.Tensor
     pca_mean: torch.Tensor
     latent_scale: float
+
+
+def load_pca_state(path: str, device: str = "cuda") -> PCAState:
+    """`load_pca_state_from_hf` (inference.py:123-137) for a LOCAL `pca_state.safetensors` (the same
+    keys: pca_components [80, 1024], pca_mean [1024], latent_scale scalar)."""
+    from safetensors.torch import load_file
+    t = load_file(path, device=device)
+    return PCAState(pca_components=t["pca_components"], pca_mean=t["pca_mean"],
+                    latent_scale=float(t["latent_scale"].item()))
+
+
+def load_model(path: str, device: str = "cuda", dtype: Optional[torch.dtype] = torch.bfloat16,
+               compile: bool = False, delete_blockwise_modules: bool = False, **kw) -> EchoDiTHip:
+    """`load_model_from_hf` (inference.py:14-69) for a LOCAL `pytorch_model.safetensors`: the HIP
+    model (model.load_model; `lora_path=` merges a reference LoRA checkpoint). `compile` is accepted
+    for signature parity: the sampler's forward is one captured hipGraph (see compile_model)."""
+    from .model import load_model as _load
+    m = _load(path, device=device, dtype=dtype, delete_blockwise_modules=delete_blockwise_modules, **kw)
+    return compile_model(m) if compile else m
+
+
+def load_fish_ae(path: str, device: str = "cuda", dtype: Optional[torch.dtype] = torch.float32,
+                 compile: bool = False):
+    """`load_fish_ae_from_hf` (inference.py:80-105) for a LOCAL Fish-S1-DAC `pytorch_model.safetensors`:
+    the HIP codec (`codec.FishAE`, decode and encode paths) over the same state-dict keys."""
+    from safetensors.torch import load_file
+    from .codec import FishAE
+    ae = FishAE(load_file(path, device="cpu"), dtype=dtype or torch.float32, device=device)
+    return compile_fish_ae(ae) if compile else ae
+
+
+def compile_fish_ae(fish_ae):
+    """inference.py:108-113 compiles the quantizer's up/down/pre/post modules; the HIP codec runs
+    them as its own kernels already, so this returns the object unchanged (signature parity)."""
+    return fish_ae
 
 
 # ---------------------------------------------------------------------------- tokenizer
@@ -101,6 +139,14 @@ def ae_decode(fish_ae, pca_state: PCAState, z_q: torch.Tensor) -> torch.Tensor:
         return fish_ae.ae_decode(pca_state, z_q)
     z = (z_q / pca_state.latent_scale) @ pca_state.pca_components + pca_state.pca_mean
     return fish_ae.decode_zq(z.transpose(1, 2).to(fish_ae.dtype)).float()
+
+
+@torch.inference_mode()
+def ae_reconstruct(fish_ae, pca_state: PCAState, audio: torch.Tensor) -> torch.Tensor:
+    """Encode then decode (inference.py:238-247)."""
+    assert audio.ndim == 3 and audio.shape[1] == 1  # (b, 1, length)
+    z_q = ae_encode(fish_ae, pca_state, audio.to(fish_ae.dtype))
+    return ae_decode(fish_ae, pca_state, z_q)
 
 
 @torch.inference_mode()

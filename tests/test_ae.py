@@ -333,3 +333,37 @@ def test_hip_speaker_latent_and_mask():
     # the batched pass equals per-chunk encodes of the same chunks
     one = ae.encoder.ae_encode(comps, mean, scale, g["audio"][:, :meta["chunk"]].unsqueeze(0).cuda())
     assert rel_l2(one.cpu(), lat[:, :one.shape[1]].cpu()) < 1e-5
+
+
+def test_load_pca_state_local(tmp_path):
+    """load_pca_state: the local form of load_pca_state_from_hf (inference.py:123-137), same keys."""
+    from safetensors.torch import save_file
+    from echo_tts_amd import inference as I
+    comps, mean, scale = CW.synthetic_pca_state()
+    p = str(tmp_path / "pca_state.safetensors")
+    save_file({"pca_components": comps, "pca_mean": mean, "latent_scale": torch.tensor(scale)}, p)
+    st = I.load_pca_state(p, device="cpu")
+    assert torch.equal(st.pca_components, comps) and torch.equal(st.pca_mean, mean)
+    assert st.latent_scale == pytest.approx(scale) and isinstance(st.latent_scale, float)
+
+
+@pytest.mark.gpu
+def test_hip_ae_reconstruct():
+    """ae_reconstruct (inference.py:238-247) through the HIP codec == the oracle's encode then decode of
+    the same clip (fp32; the encode's codes all match the reference's, test above)."""
+    from echo_tts_amd import inference as I
+    from echo_tts_amd.codec import FishAE
+    g = load_golden("ae_enc_fp32")
+    comps, mean, scale = CW.synthetic_pca_state()
+    state = CW.synthetic_encode_state()
+    state.update(CW.synthetic_decode_state())
+    ae = FishAE(state, dtype=torch.float32)
+    pca = I.PCAState(comps.cuda(), mean.cuda(), scale)
+    audio = g["audio"][:, :ENC_N["ae_enc_fp32"]].unsqueeze(0)
+    out = I.ae_reconstruct(ae, pca, audio.cuda()).cpu()
+    lat = AO.ae_encode(audio, enc_weights(torch.float32), CW.rope_table(16384), CW.rope_table(4096), comps, mean, scale)
+    ref = AO.ae_decode(lat, weights(torch.float32), cis_table(), comps, mean, scale, torch.float32)
+    assert out.shape == ref.shape
+    err = rel_l2(out, ref)
+    print(f"ae_reconstruct rel-L2 {err:.2e}")
+    assert err < 1e-3
