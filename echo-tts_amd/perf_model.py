@@ -129,3 +129,60 @@ class GemmTimer:
         return {"launches": n, "avg_ms": avg_ms, "avg_flop": avg_fl,
                 "avg_bytes": sum(r[5] for r in self.records) / n,
                 "tflops": avg_fl / (avg_ms * 1e-3) / 1e12}
+
+
+class AttnTimer:
+    """Wraps ops.attention: HIP events around every launch on the launch stream, plus its algorithmic
+    FLOPs over the VALID keys only (4·128 per (query, visible key) per head: QK^T and PV), formed
+    at summary time from the segments' length tensors (no host sync inside the run)."""
+
+    def __init__(self):
+        self.records: List = []
+        self._orig = None
+
+    def __enter__(self):
+        from . import ops
+
+        self._orig = ops.attention
+        timer = self
+
+        def wrapped(q, segments, out=None, gate=None, scale=128 ** -0.5):
+            s = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            r = timer._orig(q, segments, out=out, gate=gate, scale=scale)
+            e1.record(s)
+            R, nq, H = q.shape[0], q.shape[1], q.shape[2]
+            segs = [(sg.k.shape[1], None if sg.lens is None else sg.lens.clone(), bool(sg.causal)) for sg in segments]
+            timer.records.append((e0, e1, R, nq, H, segs))
+            return r
+
+        ops.attention = wrapped
+        return self
+
+    def __exit__(self, *exc):
+        from . import ops
+        ops.attention = self._orig
+
+    @staticmethod
+    def _flops(R, nq, H, segs) -> float:
+        keys = torch.zeros(R, dtype=torch.float64)
+        for cap, lens, causal in segs:
+            kend = (torch.full((R,), cap, dtype=torch.float64) if lens is None
+                    else lens[:R].double().cpu().clamp(min=0, max=cap))  # the kernel reads len[row], row < R
+            if causal:  # query i sees keys j <= i of the valid prefix
+                i = torch.arange(nq, dtype=torch.float64)
+                keys += torch.minimum(i[None, :] + 1, kend[:, None]).sum(1) / nq
+            else:
+                keys += kend
+        return float(4.0 * 128 * H * nq * keys.sum())
+
+    def summary(self) -> Dict[str, float]:
+        torch.cuda.synchronize()
+        n = len(self.records)
+        if n == 0:
+            return {"launches": 0}
+        ms = [a.elapsed_time(b) for a, b, *_ in self.records]
+        fl = [self._flops(*r[2:]) for r in self.records]
+        tot_ms, tot_fl = sum(ms), sum(fl)
+        return {"launches": n, "avg_ms": tot_ms / n, "avg_flop": tot_fl / n, "tflops": tot_fl / (tot_ms * 1e-3) / 1e12}
