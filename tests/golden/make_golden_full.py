@@ -23,6 +23,14 @@ equality, [4]) end to end, with the deterministic synthetic weights of
         bf16.blk2.kv_latent.{0.k,0.v,23.k,23.v}  latent-prefix KV at block 2, row 0,
                                      the 80 visible patches
         bf16.latent / fp32.latent    final [1, 640, 80] of the bf16 and fp32 runs
+  full_c5_cont.safetensors  the blockwise CONTINUATION path (`inference_blockwise.py:33-65`, the
+      second half of its __main__ example): a 317-latent continuation prefix (start_pos not a
+      multiple of 4), one 255-latent block (the reference's latent encoder needs the total length
+      to be a multiple of 4), text 203/257, speaker 301/336 valid latents,
+      CFG 3.0/3.0, truncation 0.8, temporal score rescale k=1.2 sigma=3, rng_seed 0:
+        noise0, continuation_latent
+        bf16.nfe{0,1,20,39}.{x,t,v}  teacher-forcing samples of the bf16 trajectory
+        bf16.latent / fp32.latent    final [1, 572, 80] of the bf16 and fp32 runs
 
   --truth adds, to both files, the reference's fp32 model evaluated on the bf16 run's recorded
   inputs (x and t exactly as the bf16 run fed them, bf16-rounded t included), the "truth" a
@@ -143,6 +151,81 @@ def gen_c5(ref_model, ref_blk):
         json.dump(meta, f, indent=1)
 
 
+CONT = dict(prefix=317, blocks=[255], keep=(0, 1, 20, 39))  # the reference needs (prefix + blocks) % 4 == 0
+
+
+def cont_inputs():
+    ids, tm = SY.text_inputs(1, T=257, valid=203, first_seed=1700)
+    spk, sm = SY.speaker_inputs(1, S=336, first_seed=2700)
+    sm[:, 301:] = False
+    cont = torch.randn((1, CONT["prefix"], 80), generator=torch.Generator().manual_seed(3700))
+    return ids, tm, spk, sm, cont
+
+
+def cont_kwargs():
+    return MG.sampler_kwargs(cfg_scale_speaker=3.0, truncation_factor=0.8, rescale_k=1.2, rescale_sigma=3.0)
+
+
+def gen_cont(ref_model, ref_blk):
+    ids, tm, spk, sm, cont = cont_inputs()
+    g = torch.Generator().manual_seed(0)
+    out = {"text_ids": ids, "text_mask": tm, "speaker_latent": spk, "speaker_mask": sm,
+           "continuation_latent": cont, "noise0": torch.randn((1, CONT["blocks"][0], 80), generator=g)}
+    kw = cont_kwargs()
+    meta = {"kw": kw, "blocks": CONT["blocks"], "prefix": CONT["prefix"], "seed": 0, "keep_nfe": list(CONT["keep"])}
+    for dt, tag in ((torch.bfloat16, "bf16"), (torch.float32, "fp32")):
+        t0 = time.time()
+        m, _ = MG.build_ref(ref_model, C.FULL, dt, include_latent=True)
+        rec = MG.Recorder(m)
+        with torch.inference_mode():
+            lat = ref_blk.sample_blockwise_euler_cfg_independent_guidances(m, spk, sm, ids, tm, 0, CONT["blocks"],
+                                                                           continuation_latent=cont, **kw)
+        rec.close()
+        out[f"{tag}.latent"] = lat
+        if tag == "bf16":
+            for i in CONT["keep"]:
+                x, t, v = rec.calls[i]
+                out[f"{tag}.nfe{i}.x"], out[f"{tag}.nfe{i}.t"], out[f"{tag}.nfe{i}.v"] = x, t, v
+        meta[f"{tag}_time_s"] = time.time() - t0
+        meta[f"{tag}_nfe"] = len(rec.calls)
+        del m, rec
+        print(f"CONT {tag} done in {meta[f'{tag}_time_s']:.0f}s", flush=True)
+    # the truncated x_T: the reference multiplies the block's draw by truncation_factor
+    assert torch.equal(out["bf16.nfe0.x"][:1].float(), (out["noise0"] * 0.8).to(torch.bfloat16).float())
+    save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(HERE, "full_c5_cont.safetensors"))
+    with open(os.path.join(HERE, "full_c5_cont.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+
+def gen_cont_truth(ref_model):
+    """fp32 reference forwards on the continuation bf16 trajectory's recorded inputs."""
+    from safetensors.torch import load_file
+    t0 = time.time()
+    m, _ = MG.build_ref(ref_model, C.FULL, torch.float32, include_latent=True)
+    f = os.path.join(HERE, "full_c5_cont.safetensors")
+    g = dict(load_file(f))
+    tm, sm = g["text_mask"], g["speaker_mask"]
+    start = CONT["prefix"]
+    with torch.inference_mode():
+        kvt = m.get_kv_cache_text(g["text_ids"], tm)
+        kvs = m.get_kv_cache_speaker(g["speaker_latent"])
+        prefix = torch.zeros((1, start + sum(CONT["blocks"]), 80))
+        prefix[:, :start] = g["continuation_latent"]
+        kvl1 = m.get_kv_cache_latent(prefix)
+        kvl3 = m.get_kv_cache_latent(torch.cat([prefix, prefix, prefix]))
+        for i in CONT["keep"]:
+            x, t = g[f"bf16.nfe{i}.x"].float(), g[f"bf16.nfe{i}.t"].float()
+            if x.shape[0] == 3:
+                g[f"truth32.nfe{i}.v"] = m(x=x, t=t, text_mask=torch.cat([tm, torch.zeros_like(tm), tm]),
+                                           speaker_mask=torch.cat([sm, sm, torch.zeros_like(sm)]), start_pos=start,
+                                           kv_cache_text=_cat3(kvt), kv_cache_speaker=_cat3(kvs), kv_cache_latent=kvl3)
+            else:
+                g[f"truth32.nfe{i}.v"] = m(x=x, t=t, text_mask=tm, speaker_mask=sm, start_pos=start,
+                                           kv_cache_text=kvt, kv_cache_speaker=kvs, kv_cache_latent=kvl1)
+    save_file({k: v.contiguous() for k, v in g.items()}, f)
+    print(f"CONT truth done {time.time() - t0:.0f}s", flush=True)
+
+
 def _cat3(c):
     return [(torch.cat([k, k, k]), torch.cat([v, v, v])) for k, v in c]
 
@@ -196,11 +279,16 @@ def gen_truth(ref_model, ref_inf):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", choices=("c2", "c5"), default=None)
+    ap.add_argument("--only", choices=("c2", "c5", "cont"), default=None)
     ap.add_argument("--truth", action="store_true", help="only add the fp32 teacher-forcing truth")
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count() or 8)
     ref_model, ref_inf, ref_blk = MG._import_reference()
+    if args.only == "cont":
+        if not args.truth:
+            gen_cont(ref_model, ref_blk)
+        gen_cont_truth(ref_model)
+        return
     if not args.truth:
         if args.only in (None, "c2"):
             gen_c2(ref_model, ref_inf)

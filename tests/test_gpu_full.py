@@ -61,6 +61,11 @@ def c5():
     return load_golden("full_c5_blk"), load_meta("full_c5_blk")
 
 
+@pytest.fixture(scope="module")
+def cont():
+    return load_golden("full_c5_cont"), load_meta("full_c5_cont")
+
+
 def _inputs(g):
     return tuple(g[k].to(DEV) for k in ("speaker_latent", "speaker_mask", "text_ids", "text_mask"))
 
@@ -176,10 +181,51 @@ def test_c5_engine_end_to_end_bf16(m16, c5):
     gate("C5 end-to-end bf16", lat.cpu(), g["bf16.latent"], g["fp32.latent"], 5e-3)
 
 
+# ------------------------------------------------------------------------------ blockwise continuation
+# inference_blockwise.py:58-65 + its __main__ continuation example: a 317-latent prefix (start_pos not a
+# multiple of 4), one 255-latent block, partial speaker mask, text 203/257, truncation 0.8 and the
+# temporal score rescale (k 1.2, sigma 3) — the options no other full-size case exercises.
+
+def _cont_plan(m, g, meta):
+    kw = _kw(meta)
+    sched = En.make_schedule(kw["num_steps"], kw["cfg_scale_text"], kw["cfg_scale_speaker"], kw["cfg_min_t"],
+                             kw["cfg_max_t"], kw["rescale_k"], kw["rescale_sigma"], None, None)
+    spk, sm, ids, tm = _inputs(g)
+    Tc, Pc = En.caps(m, ids, tm, spk, sm)
+    plan = En.get_block_plan(m, 1, meta["blocks"], meta["prefix"], Tc, Pc, sched, None, None)
+    return plan, (ids, tm, spk, sm), kw
+
+
+def test_cont_engine_teacher_forced_bf16(m16, cont):
+    g, meta = cont
+    plan, (ids, tm, spk, sm), kw = _cont_plan(m16, g, meta)
+    P = meta["prefix"]
+    prefix = torch.zeros((1, P + sum(meta["blocks"]), 80))
+    prefix[:, :P] = g["continuation_latent"]
+    for i in meta["keep_nfe"]:
+        plan.setup(ids, tm, spk, sm, _noise_fn(g, 1), kw["truncation_factor"],
+                   continuation=g["continuation_latent"].to(DEV))
+        v = plan.nfe(0, i, g[f"bf16.nfe{i}.x"][:1].float(), prefix.to(DEV)).cpu()
+        gate(f"CONT NFE {i}", v, g[f"bf16.nfe{i}.v"], g[f"truth32.nfe{i}.v"], 1e-3)
+
+
+def test_cont_engine_end_to_end_bf16(m16, cont):
+    g, meta = cont
+    spk, sm, ids, tm = _inputs(g)
+    kw = _kw(meta)
+    P = meta["prefix"]
+    lat = blockwise_with_noise(m16, spk, sm, ids, tm, _noise_fn(g, 1), meta["blocks"], use_graph=True,
+                               continuation_latent=g["continuation_latent"].to(DEV), **kw).cpu()
+    assert lat.shape == g["bf16.latent"].shape and torch.equal(lat[:, :P], g["continuation_latent"])
+    gate("CONT end-to-end bf16 (generated block)", lat[:, P:], g["bf16.latent"][:, P:], g["fp32.latent"][:, P:],
+         5e-3)
+
+
 # ------------------------------------------------------------------------------------------- fp32
 
-def test_fp32_end_to_end_c2_c5(c2, c5):
-    """fp32 mode at full size: final latents within 1e-3 rel-L2 of the reference's fp32 runs."""
+def test_fp32_end_to_end_c2_c5(c2, c5, cont):
+    """fp32 mode at full size: final latents within 1e-3 rel-L2 of the reference's fp32 runs (C2, C5 and
+    the blockwise continuation with truncation and score rescale)."""
     S = W.synthetic_state_dict(E.FULL, dtype=torch.float32, include_latent=True)
     m = EchoDiTHip(E.FULL, S, device=DEV, dtype=torch.float32)
     del S
@@ -190,5 +236,11 @@ def test_fp32_end_to_end_c2_c5(c2, c5):
     g5, meta5 = c5
     lat5 = blockwise_with_noise(m, spk, sm, ids, tm, _noise_fn(g5, 4), meta5["blocks"], **_kw(meta5)).cpu()
     e5 = rel_l2(lat5, g5["fp32.latent"])
-    print(f"[fp32 end-to-end] C2 {e2:.3e}  C5 {e5:.3e}")
-    assert e2 < 1e-3 and e5 < 1e-3
+    gc, metac = cont
+    spk, sm, ids, tm = _inputs(gc)
+    P = metac["prefix"]
+    latc = blockwise_with_noise(m, spk, sm, ids, tm, _noise_fn(gc, 1), metac["blocks"],
+                                continuation_latent=gc["continuation_latent"].to(DEV), **_kw(metac)).cpu()
+    ec = rel_l2(latc[:, P:], gc["fp32.latent"][:, P:])
+    print(f"[fp32 end-to-end] C2 {e2:.3e}  C5 {e5:.3e}  continuation {ec:.3e}")
+    assert e2 < 1e-3 and e5 < 1e-3 and ec < 1e-3
