@@ -159,33 +159,62 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
     bf16_t* Cp = (bf16_t*)Cv + z * sC + hcol + ch * 8;
     if (hcol >= N) return;
     constexpr int NR = PAIR ? 16 : 32;  // 4-row iterations per wave
-    for (int it = 0; it < NR; ++it) {
-      const int row = (PAIR ? (wn & 1) * 64 : 0) + it * 4 + rq;
-      const int m = m0 + wm * TM + row;
-      float v[8];
-      load8(src + row * TN + ((c ^ (row & (CHS - 1))) * 8), v);
+    // Batched: the LDS reads, RoPE table loads, sums, butterflies and reciprocal square roots of
+    // HB row iterations are issued together (independent chains interleave) instead of one
+    // row iteration's serial chain at a time; per element the same operations in the same order.
+    constexpr int HB = 4;
+    for (int it0 = 0; it0 < NR; it0 += HB) {
+      float v[HB][8];
+#pragma unroll
+      for (int b = 0; b < HB; ++b) {
+        const int row = (PAIR ? (wn & 1) * 64 : 0) + (it0 + b) * 4 + rq;
+        load8(src + row * TN + ((c ^ (row & (CHS - 1))) * 8), v[b]);
+      }
       if (norm) {
-        float ss = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) ss += v[e] * v[e];
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
-        const float r = 1.0f / sqrtf(ss / 128.0f + ep.hn_eps);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = rbf((v[e] * r) * wv[e]);
+        float4 cs[HB][2];
         if (rope) {
-          const int pos = ep.hn_pos0 + ep.hn_pos_mult * (min(m, M - 1) % ep.hn_seq_len);
-          const float* cs = ep.hn_rope + ((int64_t)pos * 64 + ch * 4) * 2;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float cc = cs[2 * e], sn = cs[2 * e + 1];
-            const float x0 = v[2 * e], x1 = v[2 * e + 1];
-            v[2 * e] = (x0 * cc) - (x1 * sn);
-            v[2 * e + 1] = (x0 * sn) + (x1 * cc);
+          for (int b = 0; b < HB; ++b) {
+            const int m = m0 + wm * TM + (PAIR ? (wn & 1) * 64 : 0) + (it0 + b) * 4 + rq;
+            const int pos = ep.hn_pos0 + ep.hn_pos_mult * (min(m, M - 1) % ep.hn_seq_len);
+            const float4* cp = (const float4*)(ep.hn_rope + ((int64_t)pos * 64 + ch * 4) * 2);
+            cs[b][0] = cp[0];
+            cs[b][1] = cp[1];
+          }
+        }
+        float ss[HB];
+#pragma unroll
+        for (int b = 0; b < HB; ++b) {
+          ss[b] = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ss[b] += v[b][e] * v[b][e];
+        }
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1)
+#pragma unroll
+          for (int b = 0; b < HB; ++b) ss[b] += __shfl_xor(ss[b], o, 64);
+#pragma unroll
+        for (int b = 0; b < HB; ++b) {
+          const float r = 1.0f / sqrtf(ss[b] / 128.0f + ep.hn_eps);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[b][e] = rbf((v[b][e] * r) * wv[e]);
+          if (rope) {
+            const float cc[4] = {cs[b][0].x, cs[b][0].z, cs[b][1].x, cs[b][1].z};
+            const float sn[4] = {cs[b][0].y, cs[b][0].w, cs[b][1].y, cs[b][1].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float x0 = v[b][2 * e], x1 = v[b][2 * e + 1];
+              v[b][2 * e] = (x0 * cc[e]) - (x1 * sn[e]);
+              v[b][2 * e + 1] = (x0 * sn[e]) + (x1 * cc[e]);
+            }
           }
         }
       }
-      if (m < M) store8(Cp + (int64_t)m * ldc, v);
+#pragma unroll
+      for (int b = 0; b < HB; ++b) {
+        const int m = m0 + wm * TM + (PAIR ? (wn & 1) * 64 : 0) + (it0 + b) * 4 + rq;
+        if (m < M) store8(Cp + (int64_t)m * ldc, v[b]);
+      }
     }
     return;
   } else if constexpr (EK != EK_GENERIC) {

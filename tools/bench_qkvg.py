@@ -39,13 +39,20 @@ def main():
             ops.head_norm_rope(out, H, qk, 1e-5, nblk=2, col0=0, col_stride=D, w_stride=H * 128, rope=rope,
                                rope_heads=H // 2, seq_len=N, pos0=0, pos_mult=1)
 
+        def store_ps():  # persistent store GEMM alone (no q/k norm): the floor for a fused epilogue
+            ops.gemm(x, w, out=out)
+
+        def store_pp2():  # the 2-phase non-persistent kernel (tile 13) with the plain store epilogue
+            ops.gemm(x, w, out=out, tile=13)
+
         fused()
         a = out.clone()
         split()
         same = bool(torch.equal(a, out))
-        times = {"fused": [], "split": []}
+        arms = (("fused", fused), ("split", split), ("store_ps", store_ps), ("store_pp2", store_pp2))
+        times = {k: [] for k, _ in arms}
         for _ in range(args.rounds):
-            for name, fn in (("fused", fused), ("split", split)):
+            for name, fn in arms:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(args.iters):
@@ -54,7 +61,8 @@ def main():
                 torch.cuda.synchronize()
                 times[name].append(e0.elapsed_time(e1) / args.iters)
         med = {k: sorted(v)[len(v) // 2] * 1e3 for k, v in times.items()}
-        print(f"M={M}: fused {med['fused']:.1f} us  split {med['split']:.1f} us  bitwise_equal={same}", flush=True)
+        print(f"M={M}: " + "  ".join(f"{k} {v:.1f} us" for k, v in med.items()) + f"  bitwise_equal={same}",
+              flush=True)
 
 
 if __name__ == "__main__":
