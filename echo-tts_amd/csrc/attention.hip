@@ -32,6 +32,18 @@ __device__ __forceinline__ float max3_f(float a, float b, float c) {
   return r;
 }
 
+// x of lane l combined with x of lane l ^ 32 through v_permlane32_swap (VALU) instead of __shfl_xor's
+// ds_bpermute (an LDS round trip on the QK -> softmax critical path): swap(x, x) gives every lane both
+// halves' values; max and + are exact and commutative, so the result equals the __shfl_xor form
+__device__ __forceinline__ float halves_max(float x) {
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+}
+__device__ __forceinline__ float halves_sum(float x) {
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+}
+
 __device__ __forceinline__ int remap_xcd(int bid, int nwg) {
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
@@ -454,7 +466,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
       for (int r = 3; r < 15; r += 2) m = max3_f(m, st[kk][r], st[kk][r + 1]);
       mx = max3_f(mx, m, st[kk][15]);
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = halves_max(mx);
     // deferred running max (cdna_hip_programming.md T13): the max moves only when some lane's
     // tile max exceeds it by more than 8 in exp2 units, so P <= 2^8 (fp32 O and l have the
     // range, a bf16 P the same relative precision) and the O rescale runs on a few tiles instead
@@ -557,7 +569,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
     st[0] = ts0; st[1] = ts1; st[2] = ts2; st[4] = ntiles; st[5] = blockIdx.x & 7;
   }
   // ---- epilogue: normalise, round, gate, store (widened 16-B accesses, attn_store_out)
-  const float lt = l_run + __shfl_xor(l_run, 32, 64);
+  const float lt = halves_sum(l_run);
   const float inv = 1.0f / lt;
   {
     const bool valid = qi < a.n_q;

@@ -81,6 +81,18 @@ __device__ __forceinline__ float silu_hw(float a) {
   return a * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(a * -1.44269504088896341f));
 }
 
+// x from lane l ^ o (o = 8, 4, 2, 1: within 16-lane rows) without ds_bpermute's LDS round trip:
+// DPP row_ror:8 for 8 ((l + 8) mod 16 = l ^ 8), quad_perm for 2 and 1, ds_swizzle (bitmask mode,
+// xor 4) for 4 — the same lane pairs as __shfl_xor, so a butterfly sum is bitwise unchanged.
+template <int O>
+__device__ __forceinline__ float xor_lane16(float x) {
+  const int v = __float_as_int(x);
+  if constexpr (O == 8) return __int_as_float(__builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false));
+  else if constexpr (O == 4) return __int_as_float(__builtin_amdgcn_ds_swizzle(v, 0x101F));
+  else if constexpr (O == 2) return __int_as_float(__builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));
+  else return __int_as_float(__builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));
+}
+
 // Epilogue shared by the bf16 kernels (must follow a barrier after the last LDS read):
 // stage 1 registers -> per-wave swizzled LDS tile (bf16-rounded, bias/act/div or SwiGLU);
 // stage 2 16-B row chunks -> residual/gate tail -> coalesced stores.
@@ -190,9 +202,13 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
           for (int e = 0; e < 8; ++e) ss[b] += v[b][e] * v[b][e];
         }
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1)
+        for (int b = 0; b < HB; ++b) ss[b] += xor_lane16<8>(ss[b]);
 #pragma unroll
-          for (int b = 0; b < HB; ++b) ss[b] += __shfl_xor(ss[b], o, 64);
+        for (int b = 0; b < HB; ++b) ss[b] += xor_lane16<4>(ss[b]);
+#pragma unroll
+        for (int b = 0; b < HB; ++b) ss[b] += xor_lane16<2>(ss[b]);
+#pragma unroll
+        for (int b = 0; b < HB; ++b) ss[b] += xor_lane16<1>(ss[b]);
 #pragma unroll
         for (int b = 0; b < HB; ++b) {
           const float r = 1.0f / sqrtf(ss[b] / 128.0f + ep.hn_eps);
