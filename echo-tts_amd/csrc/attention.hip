@@ -448,7 +448,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
     }
     float mx = -INFINITY;
     if (!(ABL & 2)) {
-    if (!full) {
+    if (!full && cpc.causal) {
 #pragma unroll
       for (int kk = 0; kk < NKK; ++kk)
 #pragma unroll
@@ -456,6 +456,17 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
           const int key = t0 + kk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
           const bool ok = key < kend && (!cpc.causal || key <= qi);
           st[kk][r] = ok ? st[kk][r] : -INFINITY;
+        }
+    } else if (!full) {
+      // prefix mask of a non-causal segment: key t0 + c + 4*h2 is visible iff 4*h2 < (kend - t0) - c,
+      // one compare of a per-lane constant with a scalar per score
+      const int lim = kend - t0, hb = 4 * h2;
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int c = kk * 32 + (r & 3) + 8 * (r >> 2);
+          st[kk][r] = hb < lim - c ? st[kk][r] : -INFINITY;
         }
     }
 #pragma unroll
