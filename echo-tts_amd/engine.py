@@ -11,6 +11,8 @@ reference computes it (so no device->host sync remains inside the loop):
 """
 from __future__ import annotations
 
+import contextlib
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
@@ -21,6 +23,13 @@ from . import ops
 from .model import EchoDiTHip, KVStore, Workspace, prefix_lengths
 
 INIT_SCALE = 0.999  # inference.py:470
+
+# Batches of at least this many latent tokens (B x N, B even) run as two half-batch plans replayed
+# concurrently on two HIP streams (`StreamSplit`); 0 disables, ECHO_STREAM_SPLIT_MIN_TOKENS overrides.
+# Measured (tools/bench_streams.py, bench.py A/B on one box; rows bitwise equal either way):
+#   C3, 16 x 640: 2 x 8 prompts 2041 ms vs 2071 ms per call (+1.5 %); 4 x 4 prompts 3.6 % slower;
+#   C5, 16 x 160-latent blocks: 2 x 8 is 6.4 % slower (M = 3840 per launch is too small to fill the chip).
+STREAM_SPLIT_MIN_TOKENS = int(os.environ.get("ECHO_STREAM_SPLIT_MIN_TOKENS", str(16 * 640)))
 
 
 @dataclass(frozen=True)
@@ -184,6 +193,9 @@ class CFGPlan:
                     self.loop()
                 self.graph = g
         self.runs += 1
+        return self.output()
+
+    def output(self) -> torch.Tensor:
         return self.x
 
     @torch.no_grad()
@@ -273,8 +285,7 @@ class BlockPlan(CFGPlan):
                 self._step(i, x, bs, seg_cfg, seg_plain, self.starts[b])
             self.prefix[:, self.starts[b]:self.starts[b] + bs].copy_(x)
 
-    def run(self, use_graph: bool) -> torch.Tensor:
-        super().run(use_graph)
+    def output(self) -> torch.Tensor:
         return self.prefix
 
     @torch.no_grad()
@@ -305,6 +316,79 @@ class BlockPlan(CFGPlan):
         return ws.v.view(copies * self.B, bs, -1).clone()
 
 
+class StreamSplit:
+    """A batch run as S sub-plans of contiguous prompt ranges whose captured graphs replay
+    concurrently on S HIP streams. Prompts are independent through the whole sampler (every kernel
+    treats rows independently and the K summation order of the GEMMs does not depend on M), so the
+    rows are bitwise those of the one-plan run; what changes is that a persistent GEMM's last,
+    partial round of tiles on one stream is filled by the other stream's work instead of idling
+    CUs (e.g. N = 2048 residual GEMMs at M = 15360: 480 tiles = 1.875 rounds of 256).
+
+    setup() takes the arguments of the sub-plans' setup with the full batch: tensors are sliced by
+    prompt; a blockwise `noise(shape)` callable is drawn for the FULL batch in the reference's
+    order (one draw per block) and each sub-plan gets its rows of every draw."""
+
+    def __init__(self, parts: List[CFGPlan]):
+        self.parts = parts
+        self.B = sum(p.B for p in parts)
+        self.bounds = []
+        s = 0
+        for p in parts:
+            self.bounds.append((s, s + p.B))
+            s += p.B
+        dev = parts[0].m.device
+        self.streams = [torch.cuda.Stream(device=dev) for _ in parts]
+
+    def setup(self, ids, text_mask, speaker_latent, speaker_mask, noise, truncation_factor, *rest):
+        if callable(noise):
+            p0 = self.parts[0]
+            draws = [noise((self.B, bs, p0.m.cfg.latent_size)) for bs in p0.blocks]
+        for p, (a, b) in zip(self.parts, self.bounds):
+            if callable(noise):
+                it = iter([d[a:b] for d in draws])
+                nz = lambda shape, it=it: next(it)  # noqa: E731
+            else:
+                nz = noise[a:b]
+            extra = [None if r is None else r[a:b] for r in rest]
+            p.setup(ids[a:b], text_mask[a:b], speaker_latent[a:b], speaker_mask[a:b], nz, truncation_factor,
+                    *extra)
+
+    def run(self, use_graph: bool) -> torch.Tensor:
+        if not use_graph or any(p.graph is None for p in self.parts):
+            for p in self.parts:        # eager, or the first (capturing) call: one stream
+                p.run(use_graph)
+        else:
+            cur = torch.cuda.current_stream()
+            for p, st in zip(self.parts, self.streams):
+                st.wait_stream(cur)
+                with torch.cuda.stream(st):
+                    p.run(True)
+            for st in self.streams:
+                cur.wait_stream(st)
+        return torch.cat([p.output() for p in self.parts])
+
+
+_single_stream = [False]
+
+
+@contextlib.contextmanager
+def single_stream():
+    """Plans made inside run the whole batch on one stream (the unsplit launch shapes: the bench's
+    roofline leg times each kernel at the config's own M)."""
+    prev = _single_stream[0]
+    _single_stream[0] = True
+    try:
+        yield
+    finally:
+        _single_stream[0] = prev
+
+
+def _split_sizes(B: int, N: int) -> Optional[Tuple[int, int]]:
+    if _single_stream[0] or STREAM_SPLIT_MIN_TOKENS <= 0 or B * N < STREAM_SPLIT_MIN_TOKENS or B % 2:
+        return None
+    return (B // 2, B // 2)
+
+
 def plan_key(B, N, Tc, Pc, sched: Schedule, kv_scale, kv_max_layers):
     return (B, N, Tc, Pc, sched, kv_scale, kv_max_layers)
 
@@ -319,13 +403,26 @@ def _cached(model: EchoDiTHip, key, make):
 
 
 def get_plan(model: EchoDiTHip, B: int, N: int, Tc: int, Pc: int, sched: Schedule,
-             kv_scale: Optional[float], kv_max_layers: Optional[int]) -> CFGPlan:
-    return _cached(model, plan_key(B, N, Tc, Pc, sched, kv_scale, kv_max_layers),
-                   lambda: CFGPlan(model, B, N, Tc, Pc, sched, kv_scale, kv_max_layers))
+             kv_scale: Optional[float], kv_max_layers: Optional[int]):
+    """The plan for one sampler shape: a `CFGPlan`, or a two-stream `StreamSplit` of two half-batch
+    CFGPlans for B x N >= STREAM_SPLIT_MIN_TOKENS (same setup/run surface)."""
+    sizes = _split_sizes(B, N)
+    if sizes is None:
+        return _cached(model, plan_key(B, N, Tc, Pc, sched, kv_scale, kv_max_layers),
+                       lambda: CFGPlan(model, B, N, Tc, Pc, sched, kv_scale, kv_max_layers))
+    return _cached(model, ("split", sizes) + plan_key(B, N, Tc, Pc, sched, kv_scale, kv_max_layers),
+                   lambda: StreamSplit([CFGPlan(model, b, N, Tc, Pc, sched, kv_scale, kv_max_layers)
+                                        for b in sizes]))
 
 
 def get_block_plan(model: EchoDiTHip, B: int, blocks, start0: int, Tc: int, Pc: int, sched: Schedule,
-                   kv_scale: Optional[float], kv_max_layers: Optional[int]) -> BlockPlan:
+                   kv_scale: Optional[float], kv_max_layers: Optional[int]):
+    """A `BlockPlan`, or a two-stream `StreamSplit` of half-batch BlockPlans (see get_plan)."""
     key = ("blockwise", tuple(blocks), start0) + plan_key(B, max(blocks), Tc, Pc, sched, kv_scale, kv_max_layers)
-    return _cached(model, key, lambda: BlockPlan(model, B, tuple(blocks), start0, Tc, Pc, sched, kv_scale,
-                                                 kv_max_layers))
+    sizes = _split_sizes(B, max(blocks))
+    if sizes is None:
+        return _cached(model, key, lambda: BlockPlan(model, B, tuple(blocks), start0, Tc, Pc, sched, kv_scale,
+                                                     kv_max_layers))
+    return _cached(model, ("split", sizes) + key,
+                   lambda: StreamSplit([BlockPlan(model, b, tuple(blocks), start0, Tc, Pc, sched, kv_scale,
+                                                  kv_max_layers) for b in sizes]))

@@ -162,6 +162,37 @@ def test_blockwise(tiny, case):
     assert e < (1e-3 if tag == "fp32" else 5e-2)
 
 
+def test_stream_split_bitwise(tiny, monkeypatch):
+    """B = 16 runs as two half-batch plans replayed concurrently on two streams (engine.StreamSplit):
+    bitwise equal to the one-stream plan of the whole batch, for the sampler and the blockwise
+    sampler (whose per-block x_T draws are made for the full batch and sliced)."""
+    from echo_tts_amd import engine as En
+    tag, dt, cfg, m, g, meta = tiny
+    monkeypatch.setattr(En, "STREAM_SPLIT_MIN_TOKENS", 1)  # split at the tiny shapes too
+    B = 16
+    rep = lambda t: t.repeat((B // t.shape[0],) + (1,) * (t.dim() - 1))  # noqa: E731
+    spk, sm, ids, tm = (rep(g[k]) for k in ("speaker_latent", "speaker_mask", "text_ids", "text_mask"))
+    kw = _kw(meta, "B")
+    noise = torch.randn((B,) + tuple(g["caseB.noise"].shape[1:]), device=DEV,
+                        generator=torch.Generator(device=DEV).manual_seed(3))
+    with En.single_stream():
+        one = sample_with_noise(m, spk, sm, ids, tm, noise, use_graph=True, **kw)
+    assert En._split_sizes(B, noise.shape[1]) == (8, 8)
+    for _ in range(3):  # eager-then-capture, then two concurrent replays
+        two = sample_with_noise(m, spk, sm, ids, tm, noise, use_graph=True, **kw)
+        assert torch.equal(one, two)
+    c = meta["blockwise"]["BLK"]
+
+    def draws():
+        gen = torch.Generator(device=DEV).manual_seed(5)
+        return lambda shape: torch.randn(shape, device=DEV, generator=gen)
+    with En.single_stream():
+        one = blockwise_with_noise(m, spk, sm, ids, tm, draws(), c["blocks"], **c["kw"])
+    for _ in range(2):
+        two = blockwise_with_noise(m, spk, sm, ids, tm, draws(), c["blocks"], **c["kw"])
+        assert torch.equal(one, two)
+
+
 def test_generic_loop_matches_engine(tiny):
     """The reference loop over EchoDiTHip's public forward/get_kv_cache_* equals the engine."""
     tag, dt, cfg, m, g, meta = tiny
