@@ -87,8 +87,8 @@ __device__ __forceinline__ float sigmoid_hw(float v) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.44269504088896341f));
 }
 
-__device__ __forceinline__ void attn_pack_out(const f32x16 (&o)[4], float inv, int h2, bool valid, const bf16_t* gp,
-                                              uint4 (&v4)[8]) {
+// normalise by 1/l, round to bf16, pack: v4[pk] = this lane's 8 columns 16*pk + 8*h2 of query ql
+__device__ __forceinline__ void attn_pack_o(const f32x16 (&o)[4], float inv, uint4 (&v4)[8]) {
   uint32_t w[16][2];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -102,14 +102,13 @@ __device__ __forceinline__ void attn_pack_out(const f32x16 (&o)[4], float inv, i
     const auto y = __builtin_amdgcn_permlane32_swap(w[2 * pk][1], w[2 * pk + 1][1], false, false);
     v4[pk] = make_uint4(x[0], y[0], x[1], y[1]);
   }
-  if (!valid || !gp) return;
-  const int c0 = 8 * h2;  // this lane's 8 columns of each 16-column pair
-  uint4 g4[8];
-#pragma unroll
-  for (int pk = 0; pk < 8; ++pk) g4[pk] = *(const uint4*)(gp + 16 * pk + c0);
-  // out = round(round(o / l) * round(sigmoid(gate))) (model.py:255-264 roundings). The precise path is
-  // needed only for gates below -87 (bf16 bits above 0xC2AE as unsigned 16-bit: negative, magnitude
-  // > 87; NaNs also land there): one packed-u16 max over the lane's 64 gates decides.
+}
+
+// out = round(round(o / l) * round(sigmoid(gate))) (model.py:255-264 roundings) on element-aligned
+// packed bf16 (v4: normalised O, g4: gates, any common layout). The precise path is needed only for
+// gates below -87 (bf16 bits above 0xC2AE as unsigned 16-bit: negative, magnitude > 87; NaNs also
+// land there): one packed-u16 max over the lane's 64 gates decides, for the whole wave.
+__device__ __forceinline__ void attn_gate(uint4 (&v4)[8], const uint4 (&g4)[8]) {
   typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
   u16x2 gmax = {0, 0};
 #pragma unroll
@@ -138,6 +137,45 @@ __device__ __forceinline__ void attn_pack_out(const f32x16 (&o)[4], float inv, i
   };
   if (__builtin_expect(__any(tiny), 0)) gated(true);
   else gated(false);
+}
+
+__device__ __forceinline__ void attn_pack_out(const f32x16 (&o)[4], float inv, int h2, bool valid, const bf16_t* gp,
+                                              uint4 (&v4)[8]) {
+  attn_pack_o(o, inv, v4);
+  if (!valid || !gp) return;
+  const int c0 = 8 * h2;  // this lane's 8 columns of each 16-column pair
+  uint4 g4[8];
+#pragma unroll
+  for (int pk = 0; pk < 8; ++pk) g4[pk] = *(const uint4*)(gp + 16 * pk + c0);
+  attn_gate(v4, g4);
+}
+
+__device__ __forceinline__ void attn_bstore(const uint4& v, __amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  typedef __attribute__((__vector_size__(4 * sizeof(unsigned int)))) unsigned int u32v4;
+  __builtin_amdgcn_raw_buffer_store_b128(u32v4{v.x, v.y, v.z, v.w}, rs, off, 0, 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t attn_rsrc(const void* p, uint32_t bytes);
+__device__ __forceinline__ void attn_bstore(const uint4& v, __amdgpu_buffer_rsrc_t rs, uint32_t off);
+
+// row-layout output of one wave (attn_bf16_kernel's epilogue): lane (rl, cc) = (lane / 16, lane % 16)
+// stores rows 4*pk + rl, columns 8*cc .. 8*cc + 7 of the wave's 32-row tile at `ob` (row stride
+// ld elements); rows >= nv fall outside the buffer range and are dropped (always 8 instructions)
+__device__ __forceinline__ void attn_store_rows(const uint4 (&v4)[8], bf16_t* ob, int nv, int64_t ld, int lane) {
+  const __amdgpu_buffer_rsrc_t rs = attn_rsrc(ob, (uint32_t)(((int64_t)(min(nv, 32) - 1) * ld + 128) * 2));
+  const uint32_t lo = (uint32_t)(((lane >> 4) * ld + (lane & 15) * 8) * 2), step = (uint32_t)(ld * 8);
+#pragma unroll
+  for (int pk = 0; pk < 8; ++pk) attn_bstore(v4[pk], rs, lo + pk * step);
+}
+
+__device__ __forceinline__ uint4 attn_bload(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  typedef __attribute__((__vector_size__(4 * sizeof(unsigned int)))) unsigned int u32v4;
+  const u32v4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t attn_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
 // 8 16-B stores per valid lane (a wave with any valid lane issues exactly 8 store instructions)
@@ -608,12 +646,50 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
       }
       (void)inv;
     } else if constexpr (PS) {
+      // (the persistent form keeps the per-lane epilogue: the row form's LDS transposition needs a
+      // barrier before the next item's DMA and spills around the item loop — 179 vs 154 us, R = 16)
       attn_pack_out(o, inv, h2, valid, gp, pend);
       pend_op = op;
       pend_valid = valid;
       pend_any = __any(valid);
+    } else if constexpr ((ABL & 2048) != 0) {
+      attn_store_out(o, inv, qi, h2, valid, op, gp);  // ablation 2048: the per-lane (32 rows x 32 B) form
     } else {
-      attn_store_out(o, inv, qi, h2, valid, op, gp);
+      // row-layout epilogue: the wave's 32 x 128 tile is transposed through its own 8 KB of LDS
+      // (free: every wave passed the last tile's barrier after its final LDS reads, and no DMA is
+      // in flight), so every gate load and output store instruction covers 4 whole 256-B rows
+      // instead of 32 rows x 32 B (cdna_hip_programming.md attention rules: "O staged through LDS
+      // and stored as whole rows"). Lane (rl, cc) = (lane / 16, lane % 16) holds rows 4*pk + rl,
+      // columns 8*cc .. 8*cc + 7. Rows past n_q: gate loads and stores fall outside the buffer ranges
+      // (loads return 0, stores are dropped).
+      const int nv = a.n_q - (q0 + w * 32);  // wave-uniform
+      if (nv > 0) {
+        const int rl = lane >> 4, cc = lane & 15;
+        const int64_t qw = q0 + w * 32;
+        uint4 g4[8];
+        auto load_gates = [&]() __attribute__((always_inline)) {
+          // rows past n_q read as 0 (outside the buffer range); their outputs are dropped below
+          const __amdgpu_buffer_rsrc_t gr =
+              attn_rsrc((const bf16_t*)a.gate + row * a.g_ld_batch + qw * a.g_ld_tok + head * 128,
+                        (uint32_t)(((int64_t)(min(nv, 32) - 1) * a.g_ld_tok + 128) * 2));
+          const uint32_t glo = (uint32_t)((rl * a.g_ld_tok + cc * 8) * 2), gst = (uint32_t)(a.g_ld_tok * 8);
+#pragma unroll
+          for (int pk = 0; pk < 8; ++pk) g4[pk] = attn_bload(gr, glo + pk * gst);
+        };
+        if (gp) load_gates();  // in flight during the transposition
+        uint4 v4[8];
+        attn_pack_o(o, inv, v4);
+        bf16_t* sw = lds + w * 32 * 128;
+#pragma unroll
+        for (int pk = 0; pk < 8; ++pk) *(uint4*)(sw + ql * 128 + (((2 * pk + h2) ^ (ql & 15)) * 8)) = v4[pk];
+#pragma unroll
+        for (int pk = 0; pk < 8; ++pk) {
+          const int r = pk * 4 + rl;
+          v4[pk] = *(const uint4*)(sw + r * 128 + ((cc ^ (r & 15)) * 8));
+        }
+        if (gp) attn_gate(v4, g4);
+        attn_store_rows(v4, (bf16_t*)a.out + row * a.o_ld_batch + qw * a.o_ld_tok + head * 128, nv, a.o_ld_tok, lane);
+      }
     }
   }
   if ((ABL & 128) && threadIdx.x == 0) {
@@ -1025,7 +1101,8 @@ int attn_ps_grid(int nitems) {
 // showed). variant: 0 production (4 waves, 2-slot LDS-DMA ring, 64-key tiles), 1/2 8 waves with
 // a 2/3-slot ring, 3/4 register-staged K/V with 4/8 waves, 5 software-pipelined kernel (two waves
 // per SIMD), 6/7 32-key tiles with a 2/3-slot ring, 8 the persistent form of 0, 9 two waves
-// (64 queries) per workgroup. ablation: the ABL bits of attn_bf16_kernel.
+// (64 queries) per workgroup, 10 = 0 with the per-lane epilogue (round-2 form before the row-layout
+// epilogue). ablation: the ABL bits of attn_bf16_kernel.
 int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) {
   const int qb = (cfg == 1 || cfg == 2 || cfg == 4) ? 256 : 128;
   const dim3 grid(attn_grid(a, qb));
@@ -1076,6 +1153,7 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       hipLaunchKernelGGL((attn_bf16_kernel<0, 2, 2>), dim3(attn_grid(a, 64)), dim3(128), 0, s, *a, (float*)nullptr, 1);
       break;
     case 7: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 3, 32); break;
+    case 10: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(2048, 4, 2); break;  // per-lane epilogue
     default: return ECHO_EINVAL;
   }
 #undef ECHO_ATTN_ABLS
@@ -1091,20 +1169,14 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   if (a->dtype == ECHO_BF16) {
-    // the persistent form (variant 8, bitwise equal) for 1-3 items per workgroup slot: there its
-    // store/prologue overlap wins (sampler R = 16: 152.7 -> 146.9 us); at more items the static
-    // item order cannot balance rows of unequal key counts the way the dispatcher does (R = 48: equal
-    // or slower), and at <= 1 item it is the same kernel
-    const int nitems = attn_grid(a, 128);
-    const int ps_grid = attn_ps_grid(nitems);
-    if (ps_grid <= 0) return ECHO_EINVAL;
+    // one workgroup per item. The persistent form (variant 8, bitwise equal; its store tail overlaps
+    // the next item's prologue) won for 1-3 items per workgroup slot with the per-lane epilogue
+    // (R = 16: 152.7 -> 146.9 us); with the row-layout epilogue the plain grid is faster there too
+    // (R = 16: 149.7 vs 153.7 us, n_q = 160: 47.7 vs 48.3, one box; profiles/r2_attn_cmp.txt).
     // (fewer items than CUs, B = 1: 64-query workgroups — variant 9, bitwise equal — are slower,
     // R = 3: 43.2 -> 54.1 us, R = 1: 38.7 -> 47.1 us: the per-workgroup tile chain stays as long and
-    // each wave issues twice the DMA; that case needs split-KV chains)
-    if (nitems > ps_grid && nitems <= 3 * ps_grid)
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a, (float*)nullptr, 1);
-    else
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(nitems), dim3(256), 0, s, *a, (float*)nullptr, 1);
+    // each wave issues twice the DMA; that case takes split-KV chains, echo_attention_split)
+    hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1);
   } else {
     hipLaunchKernelGGL(attn_f32_kernel, dim3(attn_grid(a, FQ)), dim3(64), 0, s, *a);
   }

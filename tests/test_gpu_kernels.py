@@ -407,12 +407,13 @@ def test_attention_split_kv_causal(L_):
 
 @pytest.mark.parametrize("n_q,cfg", [(640, True), (600, True), (640, False), (600, False)])
 def test_attention_persistent_multi_item(n_q, cfg):
-    """The persistent attention kernel (variant 8; production for 1-3 items per workgroup slot, e.g.
-    the sampler's R = 16 phase): with more (q block, row, head) items than its 2-per-CU grid, each
-    workgroup runs several items and stores an item's output behind the next item's loads. Bitwise
-    equal to the one-item-per-workgroup kernel (variant 0) at the sampler's shapes (R = 48 / 16),
-    with ragged text lengths (incl. 0) and, for n_q = 600, a last q block whose fourth wave has no
-    valid query (no pending stores for that wave)."""
+    """The persistent attention kernel (variant 8, per-lane epilogue): with more (q block, row, head)
+    items than its 2-per-CU grid, each workgroup runs several items and stores an item's output
+    behind the next item's loads. Bitwise equal to the one-item-per-workgroup production kernel
+    (variant 0, row-layout epilogue through LDS) and to variant 10 (variant 0 with the per-lane
+    epilogue) at the sampler's shapes (R = 48 / 16), with ragged text lengths (incl. 0) and, for
+    n_q = 600, a last q block whose third wave has 24 valid queries and fourth wave none (rows past
+    n_q: zero gate loads, and dropped stores — they would land in the next batch row's first queries)."""
     B, H, T, P = 16, 16, 448, 160
     R = 3 * B if cfg else B
     qkvg = torch.randn(R, n_q, 4, H, 128, device=DEV).to(BF)
@@ -431,6 +432,9 @@ def test_attention_persistent_multi_item(n_q, cfg):
     ops.attention_variant(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3], variant=0)
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
+    lane = torch.full_like(got, float("nan"))
+    ops.attention_variant(qkvg[:, :, 0], segs, out=lane, gate=qkvg[:, :, 3], variant=10)
+    assert torch.equal(lane, ref)
     # production (persistent or not by item count) and a repeat on the same buffers
     got.fill_(float("nan"))
     ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
