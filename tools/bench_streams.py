@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--split", type=int, default=2)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--offsets", default="0", help="comma list: spin cycles (torch.cuda._sleep) before the 2nd stream")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     import bench
@@ -62,12 +63,14 @@ def main():
             full.x.copy_(noise)
             full.graph.replay()
 
-        def run_split():
+        def run_split(off=0):
             cur = torch.cuda.current_stream()
             for j, (p, s) in enumerate(zip(parts, streams)):
                 p.x.copy_(noise[j * b:(j + 1) * b])
                 s.wait_stream(cur)
                 with torch.cuda.stream(s):
+                    if j and off:
+                        torch.cuda._sleep(off)
                     p.graph.replay()
             for s in streams:
                 cur.wait_stream(s)
@@ -79,13 +82,20 @@ def main():
             torch.cuda.synchronize()
             return time.perf_counter() - t0
 
-        tf, ts = [], []
+        offs = [int(v) for v in args.offsets.split(",")]
+        tf, ts = [], {o: [] for o in offs}
         for r in range(args.reps + 1):
-            a, c = timed(run_full), timed(run_split)
+            a = timed(run_full)
+            cs = {o: timed(lambda: run_split(o)) for o in offs}
             if r:
                 tf.append(a)
-                ts.append(c)
-            print(f"rep {r}: full B={B} {a * 1e3:.1f} ms  {S} streams x B={b} {c * 1e3:.1f} ms", flush=True)
+                for o in offs:
+                    ts[o].append(cs[o])
+            print(f"rep {r}: full B={B} {a * 1e3:.1f} ms  {S} streams x B={b}: "
+                  + "  ".join(f"off {o}: {cs[o] * 1e3:.1f} ms" for o in offs), flush=True)
+        for o in offs:
+            print(f"offset {o} cycles: split {sum(ts[o]) / len(ts[o]) * 1e3:.1f} ms  ratio {sum(ts[o]) / sum(tf):.4f}")
+        ts = ts[offs[0]]
         same = all(torch.equal(full.x[j * b:(j + 1) * b], p.x) for j, p in enumerate(parts))
         print(f"full {sum(tf) / len(tf) * 1e3:.1f} ms  split {sum(ts) / len(ts) * 1e3:.1f} ms  "
               f"ratio {sum(ts) / sum(tf):.4f}  rows_bitwise_equal={same}", flush=True)
