@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--split", type=int, default=2)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--prio", action="store_true", help="first stream at high priority (the other fills its gaps)")
     ap.add_argument("--offsets", default="0", help="comma list: spin cycles (torch.cuda._sleep) before the 2nd stream")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -57,7 +58,7 @@ def main():
             p.setup(ids[sl], tm[sl], spk[sl], sm[sl], noise[sl], None)
             p.run(True)
             parts.append(p)
-        streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
+        streams = [torch.cuda.Stream(device=dev, priority=(-1 if (args.prio and j == 0) else 0)) for j in range(S)]
 
         def run_full():
             full.x.copy_(noise)
