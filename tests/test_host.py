@@ -140,3 +140,23 @@ def test_concat_helper():
     c = [(torch.ones(1, 2), torch.zeros(1, 2))]
     out = _concat_kv_caches(c, c, c)
     assert out[0][0].shape == (3, 2)
+
+
+def test_stream_split_policy(monkeypatch):
+    """engine._split_sizes: two half-batch streams for B x N >= 16 x 640 with B even, one stream
+    otherwise, inside `single_stream()`, or when the threshold is 0 (ECHO_STREAM_SPLIT_MIN_TOKENS)."""
+    monkeypatch.setattr(En, "STREAM_SPLIT_MIN_TOKENS", 16 * 640)
+    assert En._split_sizes(16, 640) == (8, 8)
+    assert En._split_sizes(32, 640) == (16, 16)
+    assert En._split_sizes(15, 640) is None      # odd batch
+    assert En._split_sizes(8, 640) is None       # below the threshold
+    assert En._split_sizes(16, 160) is None      # blockwise 160-latent blocks at B = 16
+    assert En._split_sizes(64, 160) == (32, 32)
+    with En.single_stream():
+        assert En._split_sizes(16, 640) is None
+        with En.single_stream():
+            pass
+        assert En._split_sizes(16, 640) is None  # nested exit keeps the outer setting
+    assert En._split_sizes(16, 640) == (8, 8)
+    monkeypatch.setattr(En, "STREAM_SPLIT_MIN_TOKENS", 0)
+    assert En._split_sizes(16, 640) is None
