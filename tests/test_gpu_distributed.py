@@ -51,10 +51,12 @@ def _model():
                       dtype=torch.bfloat16)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, split=False):
     import sys
     sys.path.insert(0, REPO)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if split:  # rank 0's 2 prompts run as two concurrent 1-prompt streams (engine.StreamSplit)
+        os.environ["ECHO_STREAM_SPLIT_MIN_TOKENS"] = "1"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from echo_tts_amd import distributed as D
     torch.cuda.set_device(0)
@@ -66,11 +68,12 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_sharded_samplers_match_single_process():
+@pytest.mark.parametrize("split", [False, True])
+def test_two_rank_sharded_samplers_match_single_process(split):
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, split)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
