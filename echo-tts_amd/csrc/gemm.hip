@@ -1475,6 +1475,8 @@ int launch_pp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 }
 
 int g_gemm_stagger = 0;  // echo_gemm_set_diag key 1
+int g_gemm_no_rowsplit = 0;  // key 3: no row-tail split of 256x256 launches (A/B)
+int g_gemm_no_ps = 0;        // key 4: the 2-phase kernel instead of the persistent one (A/B)
 
 }  // namespace
 
@@ -1482,6 +1484,8 @@ extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   if (value < 0) return ECHO_EINVAL;
   if (key == 1) g_gemm_stagger = value;
   else if (key == 2) g_gemm_ns3 = value != 0;
+  else if (key == 3) g_gemm_no_rowsplit = value != 0;
+  else if (key == 4) g_gemm_no_ps = value != 0;
   else return ECHO_EINVAL;
   return 0;
 }
@@ -1524,7 +1528,7 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   int t = a->tile > 0 ? a->tile : pick_tile(a->M, a->N, a->K, a->batch);
   // 256x256 tiles run the persistent 2-phase kernel where its register epilogue applies, else the
   // 2-phase ping-pong (all bitwise-identical results)
-  if (a->tile == 0 && t == 1) t = (a->dtype == ECHO_BF16 && ps_ok(a, ek_of(a))) ? 16 : 13;
+  if (a->tile == 0 && t == 1) t = (a->dtype == ECHO_BF16 && ps_ok(a, ek_of(a)) && !g_gemm_no_ps) ? 16 : 13;
   if (headnorm && (a->dtype != ECHO_BF16 || t != 13 || a->N % 128)) {
     // not fused for this shape / dtype: plain store, then the standalone kernel (same results)
     EchoGemmArgs b = *a;
@@ -1554,7 +1558,7 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
   if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C) & 15) return ECHO_EALIGN;
   int tail_cfg = 0;
-  const int M1 = (a->tile == 0 && (t == 13 || t == 16) && a->batch == 1 && !headnorm)
+  const int M1 = (a->tile == 0 && (t == 13 || t == 16) && a->batch == 1 && !headnorm && !g_gemm_no_rowsplit)
                      ? split_rows(a->M, a->N, &tail_cfg) : 0;
   if (M1 > 0) {
     // two launches on the same stream: full rounds of the 256x256 kernel, then the row tail

@@ -89,7 +89,9 @@ int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch);
  * between the 8 first-round workgroup groups of an XCD for `tile` = 14 (the 256x256 kernel with
  * staggered tile rounds), in 10 ns ticks; also the persistent kernel's group-M height for
  * `tile` = 18. key 2: 0 turns the 3-stage pipeline of the two smallest tile configs off (A/B
- * timing; both schedules give bitwise-equal results). */
+ * timing; both schedules give bitwise-equal results). key 3: 1 = no row-tail split of auto-picked
+ * 256x256 launches; key 4: 1 = the 2-phase kernel instead of the persistent one for auto-picked
+ * 256x256 launches (A/B timing, tools/bench_streams.py --diag; all bitwise-equal). */
 int echo_gemm_set_diag(int32_t key, int32_t value);
 
 /* One key/value segment of the joint attention (model.py:246-253): rows of

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--split", type=int, default=2)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--diag", default="", help="echo_gemm_set_diag key=value,... applied before any plan")
     ap.add_argument("--prio", action="store_true", help="first stream at high priority (the other fills its gaps)")
     ap.add_argument("--offsets", default="0", help="comma list: spin cycles (torch.cuda._sleep) before the 2nd stream")
     args = ap.parse_args()
@@ -35,6 +36,11 @@ def main():
     from echo_tts_amd.model import EchoDiTHip
 
     cfg = EA.FULL
+    if args.diag:
+        from echo_tts_amd import ops
+        for kv in args.diag.split(","):
+            k, v = (int(t) for t in kv.split("="))
+            assert ops.lib().echo_gemm_set_diag(k, v) == 0
     state = W.fast_random_state_dict(cfg, str(dev), torch.bfloat16, seed=1234, include_latent=False)
     model = EchoDiTHip(cfg, state, device=dev, dtype=torch.bfloat16)
     del state
