@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--split", type=int, default=2)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--cfg-min-t", type=float, default=None, help="override cfg_min_t (0: all CFG steps, 2: none)")
     ap.add_argument("--diag", default="", help="echo_gemm_set_diag key=value,... applied before any plan")
     ap.add_argument("--prio", action="store_true", help="first stream at high priority (the other fills its gaps)")
     ap.add_argument("--offsets", default="0", help="comma list: spin cycles (torch.cuda._sleep) before the 2nd stream")
@@ -47,6 +48,8 @@ def main():
     B, S = args.batch, args.split
     ids, tm, spk, sm = (t.to(dev) for t in bench.global_inputs(B))
     kw = {k: v for k, v in bench.SAMPLER_KW.items() if k != "sequence_length"}
+    if args.cfg_min_t is not None:
+        kw["cfg_min_t"] = args.cfg_min_t
     sched = E.make_schedule(kw["num_steps"], kw["cfg_scale_text"], kw["cfg_scale_speaker"], kw["cfg_min_t"],
                             kw["cfg_max_t"], None, None, None, None)
     Tc, Pc = E.caps(model, ids, tm, spk, sm)
