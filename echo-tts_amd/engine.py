@@ -168,7 +168,8 @@ class CFGPlan:
         copies = 3 if cfg_step else 1
         ws = self.ws.view(copies * self.B * N)
         ops.latent_to_input(x, ws.xin, copies)
-        self.m.decoder(ws, copies * self.B, N, self.table[i], segs_cfg if cfg_step else segs_plain, start_pos)
+        self.m.decoder(ws, copies * self.B, N, self.table[i], segs_cfg if cfg_step else segs_plain, start_pos,
+                       copies=copies)
         ops.euler_step(x, ws.v, self.args[i])
         if self.sched.unscale_step == i and self.kv_scale is not None:
             self._scale_speaker(1.0 / self.kv_scale)
@@ -210,7 +211,7 @@ class CFGPlan:
         ws = self.ws.view(copies * self.B * self.N)
         ops.latent_to_input(xs, ws.xin, copies)
         seg = self._segs(self.sched.has_cfg[i])
-        self.m.decoder(ws, copies * self.B, self.N, self.table[i], seg, 0)
+        self.m.decoder(ws, copies * self.B, self.N, self.table[i], seg, 0, copies=copies)
         return ws.v.view(copies * self.B, self.N, -1).clone()
 
 
@@ -312,7 +313,7 @@ class BlockPlan(CFGPlan):
         ws = self.ws.view(copies * self.B * bs)
         ops.latent_to_input(xs, ws.xin, copies)
         self.m.decoder(ws, copies * self.B, bs, self.table[i], seg_cfg if self.sched.has_cfg[i] else seg_plain,
-                       self.starts[b])
+                       self.starts[b], copies=copies)
         return ws.v.view(copies * self.B, bs, -1).clone()
 
 

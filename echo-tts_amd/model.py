@@ -15,6 +15,7 @@ kv_cache_latent)`, `get_kv_cache_text/speaker/latent`, `__call__` = forward.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -27,6 +28,8 @@ from .config import EchoConfig
 
 Tensor = torch.Tensor
 MAX_POS = 8192  # RoPE table rows: decoder start_pos + N, encoder lengths, latent positions 4j
+# decoder(copies > 1): layer 0's AdaLN + QKVG on one row group (ECHO_SHARE_LAYER0=0 disables, A/B runs)
+SHARE_LAYER0 = os.environ.get("ECHO_SHARE_LAYER0", "1") != "0"
 IN_PAD = 128    # in_proj reduction dim padded from 80 (zero columns contribute exact zeros)
 
 
@@ -376,12 +379,16 @@ class EchoDiTHip:
         return self._ws.view(rows)
 
     def decoder(self, ws: Workspace, R: int, N: int, tab: Tensor, segs, start_pos: int = 0,
-                per_row_tab: bool = False) -> Tensor:
+                per_row_tab: bool = False, copies: int = 1) -> Tensor:
         """EchoDiT.forward body (model.py:575-604) on ws.xin [R*N, 128] -> ws.v [R*N, 80] fp32.
 
         tab: [2L, 3, D] (one timestep for all rows) or [R, 2L, 3, D] with per_row_tab.
         segs: [latent, text, speaker] segments (None = absent) shared by all layers, or a
         callable layer -> such a list; self-attention keys come from ws.qkvg.
+        copies: the rows are `copies` identical groups of R / copies (the CFG batch, inference.py:516:
+        the same x three times). Layer 0's AdaLN and QKVG projection then run on one group only —
+        its Q/K/V/gate are the same for every group — and its attention runs once per group with
+        that group's text/speaker lengths (bitwise equal to the full computation).
         """
         cfg = self.cfg
         D, H, eps = cfg.model_size, cfg.num_heads, cfg.norm_eps
@@ -393,6 +400,8 @@ class EchoDiTHip:
         self_seg = ops.Segment(q4[:, :, 1], q4[:, :, 2])
         og4 = ws.og.view(R, N, H, 128)
         shared = None if callable(segs) else [self_seg] + [s for s in segs if s is not None]
+        share0 = copies > 1 and not per_row_tab and SHARE_LAYER0 and R % copies == 0
+        Rg = R // copies if share0 else R
         for i, lay in enumerate(self.layers):
             all_segs = shared if shared is not None else [self_seg] + [s for s in segs(i) if s is not None]
             for a in range(2):
@@ -400,8 +409,23 @@ class EchoDiTHip:
                     sh, s1, g = tab[:, 2 * i + a, 0], tab[:, 2 * i + a, 1], tab[:, 2 * i + a, 2]
                 else:
                     sh, s1, g = tab[2 * i + a, 0], tab[2 * i + a, 1], tab[2 * i + a, 2]
-                ops.adaln_modulate(ws.h, sh, s1, eps, ws.xn)
-                if a == 0:
+                if a == 0 and i == 0 and share0:
+                    # layer 0 of identical row groups: AdaLN + QKVG on the first group only
+                    Mg = Rg * N
+                    ops.adaln_modulate(ws.h[:Mg], sh, s1, eps, ws.xn[:Mg])
+                    ops.gemm(ws.xn[:Mg], lay.wqkvg, out=ws.qkvg[:Mg],
+                             head_norm=ops.HeadNorm(lay.qk_norm, H, 2, eps, w_stride=H * 128, rope=self.rope,
+                                                    rope_heads=H // 2, seq_len=N, pos0=start_pos))
+                    qg = ws.qkvg[:Mg].view(Rg, N, 4, H, 128)
+                    for c in range(copies):
+                        gs = [ops.Segment(qg[:, :, 1], qg[:, :, 2])]
+                        for sg in all_segs[1:]:
+                            gs.append(ops.Segment(sg.k, sg.v, None if sg.lens is None else sg.lens[c * Rg:(c + 1) * Rg],
+                                                  sg.batch_mod, sg.causal))
+                        ops.attention(qg[:, :, 0], gs, out=og4[c * Rg:(c + 1) * Rg], gate=qg[:, :, 3])
+                    src, w = ws.og, lay.wo
+                elif a == 0:
+                    ops.adaln_modulate(ws.h, sh, s1, eps, ws.xn)
                     # QKVG projection with q/k RMSNorm + half RoPE fused into its epilogue
                     ops.gemm(ws.xn, lay.wqkvg, out=ws.qkvg,
                              head_norm=ops.HeadNorm(lay.qk_norm, H, 2, eps, w_stride=H * 128, rope=self.rope,
@@ -409,6 +433,7 @@ class EchoDiTHip:
                     ops.attention(q4[:, :, 0], all_segs, out=og4, gate=q4[:, :, 3])
                     src, w = ws.og, lay.wo
                 else:
+                    ops.adaln_modulate(ws.h, sh, s1, eps, ws.xn)
                     ops.gemm(ws.xn, lay.w13, out=ws.u, epilogue=L.EPI_SWIGLU)
                     src, w = ws.u, lay.w2
                 if per_row_tab:

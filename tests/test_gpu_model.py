@@ -193,6 +193,27 @@ def test_stream_split_bitwise(tiny, monkeypatch):
         assert torch.equal(one, two)
 
 
+def test_share_layer0_bitwise(tiny, monkeypatch):
+    """CFG steps run layer 0's AdaLN + QKVG on one of the three identical row groups and its attention
+    once per group (model.decoder(copies=3)): bitwise equal to the full computation, for the sampler
+    (case B: speaker-KV scale, rescale) and the blockwise sampler (latent segment)."""
+    from echo_tts_amd import model as Mo
+    tag, dt, cfg, m, g, meta = tiny
+    kw = _kw(meta, "B")
+    args = (m, g["speaker_latent"], g["speaker_mask"], g["text_ids"], g["text_mask"], g["caseB.noise"])
+    c = meta["blockwise"]["BLK"]
+
+    def blk():
+        noises = iter([g[f"caseBLK.noise{j}"] for j in range(len(c["blocks"]))])
+        return blockwise_with_noise(m, g["speaker_latent"], g["speaker_mask"], g["text_ids"], g["text_mask"],
+                                    lambda shape: next(noises), c["blocks"], use_graph=False, **c["kw"])
+    monkeypatch.setattr(Mo, "SHARE_LAYER0", True)
+    on, on_blk = sample_with_noise(*args, use_graph=False, **kw), blk()
+    monkeypatch.setattr(Mo, "SHARE_LAYER0", False)
+    off, off_blk = sample_with_noise(*args, use_graph=False, **kw), blk()
+    assert torch.equal(on, off) and torch.equal(on_blk, off_blk)
+
+
 def test_generic_loop_matches_engine(tiny):
     """The reference loop over EchoDiTHip's public forward/get_kv_cache_* equals the engine."""
     tag, dt, cfg, m, g, meta = tiny
