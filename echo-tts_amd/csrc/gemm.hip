@@ -1284,6 +1284,8 @@ double tile_cost(int c, int M, int N, int batch) {
   return rounds * t.occ * (double)t.bm * t.bn / t.eff;
 }
 
+int g_gemm_fill_min = 128;  // echo_gemm_set_diag key 5: a 256x256 pick below this many tiles switches (A/B)
+
 int pick_tile(int M, int N, int K, int batch) {
   (void)K;
   int best = 1;
@@ -1299,7 +1301,7 @@ int pick_tile(int M, int N, int K, int batch) {
   // big tile still wins (C5 decoder, N=2048 residual: M=7680 / 240 tiles 59.8 vs 74.5 us on 128x128,
   // M=5120 / 160 tiles 48.3 vs 55.9 us; M=2560 / 80 tiles 45.3 vs 33.3 us): its switch is below 128
   auto ntiles = [&](int c) { return (double)((M + kTiles[c].bm - 1) / kTiles[c].bm) * ((N + kTiles[c].bn - 1) / kTiles[c].bn) * batch; };
-  if (ntiles(best - 1) < (best == 1 ? 128 : 256)) {
+  if (ntiles(best - 1) < (best == 1 ? g_gemm_fill_min : 256)) {
     for (int c = 2; c < 5; ++c)
       if (ntiles(c) >= 256 || c == 4) return c + 1;
   }
@@ -1486,6 +1488,7 @@ extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   else if (key == 2) g_gemm_ns3 = value != 0;
   else if (key == 3) g_gemm_no_rowsplit = value != 0;
   else if (key == 4) g_gemm_no_ps = value != 0;
+  else if (key == 5) g_gemm_fill_min = value;
   else return ECHO_EINVAL;
   return 0;
 }

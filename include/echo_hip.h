@@ -91,7 +91,8 @@ int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch);
  * `tile` = 18. key 2: 0 turns the 3-stage pipeline of the two smallest tile configs off (A/B
  * timing; both schedules give bitwise-equal results). key 3: 1 = no row-tail split of auto-picked
  * 256x256 launches; key 4: 1 = the 2-phase kernel instead of the persistent one for auto-picked
- * 256x256 launches (A/B timing, tools/bench_streams.py --diag; all bitwise-equal). */
+ * 256x256 launches; key 5: tile count below which an auto-picked 256x256 launch switches to a
+ * smaller tile (default 128) (A/B timing, tools/bench_streams.py --diag; all bitwise-equal). */
 int echo_gemm_set_diag(int32_t key, int32_t value);
 
 /* One key/value segment of the joint attention (model.py:246-253): rows of
