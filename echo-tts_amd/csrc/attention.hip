@@ -260,7 +260,8 @@ struct SegInfo {
 // T14): tile t+2 is loaded into VGPRs at the top of tile t and written (swizzled) into the free LDS
 // buffer at the top of tile t+1, so 2 LDS buffers give a 2-tile lookahead.
 //
-// PS = 1: persistent form of the production schedule — gridDim.x workgroups walk the (q block, row,
+// PS = 1 (variant 8; production for 1-3 items per slot until the row-layout epilogue made the plain
+// grid faster): persistent form of the production schedule — gridDim.x workgroups walk the (q block, row,
 // head) items item = blockIdx.x + k * gridDim.x (same XCD for every k when gridDim.x % 8 == 0). An
 // item's gated output is stored after the NEXT item's Q loads and first K/V DMA have been issued, and
 // only those are waited for (vmcnt counts loads, LDS-DMA and stores in issue order), so the store
