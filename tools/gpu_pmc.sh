@@ -5,6 +5,8 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift
 export TMPDIR=/tmp
+# one stream: the counted launches have the config's own shapes (those the bench's roofline leg times)
+export ECHO_STREAM_SPLIT_MIN_TOKENS=0
 cd /tmp || exit 1
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 ${PMC_TIMEOUT:-600} rocprofv3 --pmc $C --kernel-include-regex "${KREGEX:-gemm_bf16_(ps|pp2)_kernel}" --output-format csv \
