@@ -1284,6 +1284,7 @@ double tile_cost(int c, int M, int N, int batch) {
   return rounds * t.occ * (double)t.bm * t.bn / t.eff;
 }
 
+int g_gemm_ps_grid = 0;     // echo_gemm_set_diag key 6: persistent-kernel workgroup count cap (0 = CUs; A/B)
 int g_gemm_fill_min = 128;  // echo_gemm_set_diag key 5: a 256x256 pick below this many tiles switches (A/B)
 
 int pick_tile(int M, int N, int K, int batch) {
@@ -1395,7 +1396,7 @@ int launch_ps_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
     if (n <= 0) return ECHO_EINVAL;
     g_num_cus = n;
   }
-  const int grid = min(tm * tn, g_num_cus);
+  const int grid = min(tm * tn, g_gemm_ps_grid > 0 ? g_gemm_ps_grid : g_num_cus);
   // group-M height 8. Measured with tile 18 (tools/bench_gemm.py --stagger G): 1, 2, 4 and 16 are
   // 2-6 % slower on QKVG/W13; on the N = 2048 residual GEMMs 4 was within +-2 % of 8 in either
   // direction across two boxes (Wo 245 vs 252 / 235 vs 229 us, W2 591 vs 604 / 579 vs 587 us)
@@ -1489,6 +1490,7 @@ extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   else if (key == 3) g_gemm_no_rowsplit = value != 0;
   else if (key == 4) g_gemm_no_ps = value != 0;
   else if (key == 5) g_gemm_fill_min = value;
+  else if (key == 6) g_gemm_ps_grid = value;
   else return ECHO_EINVAL;
   return 0;
 }
