@@ -39,12 +39,12 @@ def test_host_code_under_asan(tmp_path):
     if not os.path.exists(clang):
         clang = "/opt/rocm/lib/llvm/bin/clang"
     drv = str(tmp_path / "asan_host.o")
-    r = subprocess.run([clang, "-O1", "-g", "-fsanitize=address", "-fno-omit-frame-pointer", "-c",
+    r = subprocess.run([clang, "-O1", "-g", "-fsanitize=address", "-fno-gpu-sanitize", "-fno-omit-frame-pointer", "-c",
                         os.path.join(REPO, "tools", "asan_host.c"), "-o", drv], capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     exe = str(tmp_path / "asan_host")
-    r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-fsanitize=address", "-o", exe, drv, *objs],
+    r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-fsanitize=address", "-fno-gpu-sanitize", "-o", exe, drv, *objs],
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:halt_on_error=1",
