@@ -50,7 +50,7 @@ class AttnArgs(C.Structure):
                 ("q", vp), ("q_ld_tok", i64), ("q_ld_batch", i64),
                 ("gate", vp), ("g_ld_tok", i64), ("g_ld_batch", i64),
                 ("out", vp), ("o_ld_tok", i64), ("o_ld_batch", i64),
-                ("scale", f32), ("seg", KVSegment * 4)]
+                ("scale", f32), ("seg", KVSegment * 4), ("q_batch_mod", i32)]
 
 
 class StepArgs(C.Structure):

@@ -21,6 +21,9 @@
 
 #include <type_traits>
 
+// q / gate row of output row `row` (EchoAttnArgs.q_batch_mod: row groups that share one q copy)
+#define ECHO_QROW(a, row) ((a).q_batch_mod > 0 ? (row) % (a).q_batch_mod : (row))
+
 namespace {
 
 __device__ __forceinline__ int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
@@ -79,14 +82,6 @@ __device__ __forceinline__ T sel4(int sg, T a0, T a1, T a2, T a3) {
 // 32-63 columns 8k+8 .. 8k+15, so gate loads and output stores are 16 B per lane (8 + 8 instead of
 // 16 + 16 8-B accesses; the store tail is issue-bound). Same roundings as the reference
 // (model.py:255-264: SDPA out bf16, sigmoid(gate) bf16, product bf16).
-// sigmoid from the hardware v_exp_f32 / v_rcp_f32 (≈3 ulp fp32): rounded to bf16 it equals the rounded
-// precise fp32 sigmoid (expf + IEEE division) for every bf16 input except the three whose results are
-// fp32 denormals (x = -87.5, -88, -88.5: the hardware ops flush them to 0) — checked exhaustively over all
-// 65536 inputs on MI355X (tools/sigmoid_exhaustive.hip). Callers take the precise path for x < -87.
-__device__ __forceinline__ float sigmoid_hw(float v) {
-  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.44269504088896341f));
-}
-
 // normalise by 1/l, round to bf16, pack: v4[pk] = this lane's 8 columns 16*pk + 8*h2 of query ql
 __device__ __forceinline__ void attn_pack_o(const f32x16 (&o)[4], float inv, uint4 (&v4)[8]) {
   uint32_t w[16][2];
@@ -319,7 +314,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
   const int qi = q0 + w * 32 + ql;
   const int qc = min(qi, a.n_q - 1);
 
-  const bf16_t* qp = (const bf16_t*)a.q + row * a.q_ld_batch + (int64_t)qc * a.q_ld_tok + head * 128;
+  const bf16_t* qp = (const bf16_t*)a.q + ECHO_QROW(a, row) * a.q_ld_batch + (int64_t)qc * a.q_ld_tok + head * 128;
   bf16x8 qf[8];
 #pragma unroll
   for (int ds = 0; ds < 8; ++ds) qf[ds] = *(const bf16x8*)(qp + 16 * ds + 8 * h2);
@@ -624,7 +619,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
   {
     const bool valid = qi < a.n_q;
     bf16_t* op = (bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qc * a.o_ld_tok + head * 128;
-    const bf16_t* gp = a.gate ? (const bf16_t*)a.gate + row * a.g_ld_batch + (int64_t)qc * a.g_ld_tok + head * 128
+    const bf16_t* gp = a.gate ? (const bf16_t*)a.gate + ECHO_QROW(a, row) * a.g_ld_batch + (int64_t)qc * a.g_ld_tok + head * 128
                               : nullptr;
     if constexpr (SP) {
       // partial O at chunk c = d / 4 (32 chunks of 4 floats), laid out [chunk][query] so the 32
@@ -671,7 +666,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
         auto load_gates = [&]() __attribute__((always_inline)) {
           // rows past n_q read as 0 (outside the buffer range); their outputs are dropped below
           const __amdgpu_buffer_rsrc_t gr =
-              attn_rsrc((const bf16_t*)a.gate + row * a.g_ld_batch + qw * a.g_ld_tok + head * 128,
+              attn_rsrc((const bf16_t*)a.gate + ECHO_QROW(a, row) * a.g_ld_batch + qw * a.g_ld_tok + head * 128,
                         (uint32_t)(((int64_t)(min(nv, 32) - 1) * a.g_ld_tok + 128) * 2));
           const uint32_t glo = (uint32_t)((rl * a.g_ld_tok + cc * 8) * 2), gst = (uint32_t)(a.g_ld_tok * 8);
 #pragma unroll
@@ -733,7 +728,7 @@ __global__ void __launch_bounds__(256, 2) attn_pipe_kernel(EchoAttnArgs a) {
   const int qi = q0 + w * 32 + ql;
   const int qc = min(qi, a.n_q - 1);
 
-  const bf16_t* qp = (const bf16_t*)a.q + row * a.q_ld_batch + (int64_t)qc * a.q_ld_tok + head * 128;
+  const bf16_t* qp = (const bf16_t*)a.q + ECHO_QROW(a, row) * a.q_ld_batch + (int64_t)qc * a.q_ld_tok + head * 128;
   bf16x8 qf[8];
 #pragma unroll
   for (int ds = 0; ds < 8; ++ds) qf[ds] = *(const bf16x8*)(qp + 16 * ds + 8 * h2);
@@ -923,7 +918,7 @@ __global__ void __launch_bounds__(256, 2) attn_pipe_kernel(EchoAttnArgs a) {
   const float inv = 1.0f / lt;
   if (qi >= a.n_q) return;
   bf16_t* op = (bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qi * a.o_ld_tok + head * 128;
-  const bf16_t* gp = a.gate ? (const bf16_t*)a.gate + row * a.g_ld_batch + (int64_t)qi * a.g_ld_tok + head * 128
+  const bf16_t* gp = a.gate ? (const bf16_t*)a.gate + ECHO_QROW(a, row) * a.g_ld_batch + (int64_t)qi * a.g_ld_tok + head * 128
                             : nullptr;
   uint2 gg[16];
   if (gp) {
@@ -981,7 +976,7 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(EchoAttnArgs a, const
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = rbf(acc[e] * inv);
   if (a.gate) {
-    const uint4 g4 = *(const uint4*)((const bf16_t*)a.gate + row * a.g_ld_batch + (int64_t)qi * a.g_ld_tok + head * 128 +
+    const uint4 g4 = *(const uint4*)((const bf16_t*)a.gate + ECHO_QROW(a, row) * a.g_ld_batch + (int64_t)qi * a.g_ld_tok + head * 128 +
                                      8 * c8);
     const uint32_t gg[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
@@ -1005,7 +1000,7 @@ __global__ void __launch_bounds__(64) attn_f32_kernel(EchoAttnArgs a) {
   const int qb = L % nqb, head = (L / nqb) % a.heads, row = L / (nqb * a.heads);
   const int tid = threadIdx.x;
   const int qi = qb * FQ + tid, qc = min(qi, a.n_q - 1);
-  const float* qp = (const float*)a.q + row * a.q_ld_batch + (int64_t)qc * a.q_ld_tok + head * 128;
+  const float* qp = (const float*)a.q + ECHO_QROW(a, row) * a.q_ld_batch + (int64_t)qc * a.q_ld_tok + head * 128;
   float q[128], o[128];
 #pragma unroll
   for (int d = 0; d < 128; ++d) { q[d] = qp[d]; o[d] = 0.f; }
@@ -1049,7 +1044,7 @@ __global__ void __launch_bounds__(64) attn_f32_kernel(EchoAttnArgs a) {
   }
   if (qi >= a.n_q) return;
   float* op = (float*)a.out + row * a.o_ld_batch + (int64_t)qi * a.o_ld_tok + head * 128;
-  const float* gp = a.gate ? (const float*)a.gate + row * a.g_ld_batch + (int64_t)qi * a.g_ld_tok + head * 128
+  const float* gp = a.gate ? (const float*)a.gate + ECHO_QROW(a, row) * a.g_ld_batch + (int64_t)qi * a.g_ld_tok + head * 128
                            : nullptr;
 #pragma unroll
   for (int d = 0; d < 128; ++d) {
@@ -1066,6 +1061,7 @@ namespace {
 int check_attn_args(const EchoAttnArgs* a) {
   if (!a || !a->q || !a->out) return ECHO_EINVAL;
   if (a->rows <= 0 || a->n_q <= 0 || a->heads <= 0 || a->nseg < 1 || a->nseg > 4) return ECHO_ESHAPE;
+  if (a->q_batch_mod < 0 || a->q_batch_mod > a->rows) return ECHO_ESHAPE;
   bool any = false;
   for (int s = 0; s < a->nseg; ++s) {
     const EchoKVSegment& S = a->seg[s];

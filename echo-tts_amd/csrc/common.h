@@ -64,6 +64,31 @@ __device__ __forceinline__ void store8(float* p, const float* v) {
 __device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
 __device__ __forceinline__ float sigmoid_f(float v) { return 1.0f / (1.0f + expf(-v)); }
 
+// Hardware-op forms of sigmoid / SiLU for bf16 INPUTS (v_exp_f32 + v_rcp_f32 instead of expf + IEEE
+// division), each checked over all 65536 bf16 inputs on MI355X against the precise fp32 form the
+// reference's bf16 ops compute (tools/sigmoid_exhaustive.hip includes this header, so it tests these
+// exact functions; profiles/r3_sigmoid_exhaustive.txt).
+//
+// sigmoid_hw (attention gate, model.py:157,264): rounded to bf16 it equals the rounded precise
+// sigmoid for every input except x = -87.5, -88, -88.5, whose sigmoids are fp32 denormals that
+// v_rcp_f32 flushes to 0. Callers take the precise path for x < -87 (a wave-uniform rare branch).
+__device__ __forceinline__ float sigmoid_hw(float v) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.44269504088896341f));
+}
+// silu_bf16in (SwiGLU epilogue, model.py:307): rbf(silu_bf16in(a)) == rbf(a / (1 + expf(-a))) for
+// every bf16 a, by two fix-ups of the hardware form a * rcp(1 + 2^(-a log2 e)):
+//  * a < -64: numerator and divisor are scaled by 2^-32 (exact) so that the reciprocal of the huge
+//    1 + e^-a stays normal — otherwise v_rcp_f32 flushes it and a in {-87.5, -88, -88.5}, whose
+//    SiLUs are normal numbers (~-8.7e-37), come out as -0;
+//  * a = 5.9375: its fp32 SiLU, 5.9218745, lies one fp32 ulp below the bf16 rounding midpoint
+//    5.921875 that the ~2-ulp hardware form crosses; the exact bf16 result 5.90625 is selected.
+__device__ __forceinline__ float silu_bf16in(float a) {
+  const float sc = a < -64.0f ? 0x1p-32f : 1.0f;
+  const float d = 1.0f + __builtin_amdgcn_exp2f(a * -1.44269504088896341f);
+  const float s = (a * sc) * __builtin_amdgcn_rcpf(d * sc);
+  return a == 5.9375f ? 5.90625f : s;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

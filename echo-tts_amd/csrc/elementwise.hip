@@ -189,9 +189,13 @@ __global__ void temb_kernel(const float* __restrict__ t, const float* __restrict
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= S * half) return;
   const int s = i / half, k = i % half;
+  // args = t * freqs in fp32 (model.py:40); cos / sin of that fp32 value correctly rounded to fp32
+  // (fp64 evaluation) before the dtype rounding, so the embedding does not depend on the device
+  // cosf / sinf accuracy at arguments up to 1000 rad (the reference's <= 1-ulp fp32 cos / sin round to
+  // the same bf16 as the correctly rounded values for the schedules tested, tools/diag_adaln_stages.py).
   const float a = t[s] * freqs[k];
-  Elt<T>::st(out + (int64_t)s * 2 * half + k, cosf(a));
-  Elt<T>::st(out + (int64_t)s * 2 * half + half + k, sinf(a));
+  Elt<T>::st(out + (int64_t)s * 2 * half + k, (float)cos((double)a));
+  Elt<T>::st(out + (int64_t)s * 2 * half + half + k, (float)sin((double)a));
 }
 
 template <typename T>

@@ -75,12 +75,6 @@ __device__ __forceinline__ float epi_pointwise(float v, const Epi& ep, int n) {
 // EK_BIAS (store + bias, the decoder's input projection) exists in the persistent kernel only.
 enum { EK_GENERIC = 0, EK_STORE = 1, EK_SWIGLU = 2, EK_RESID = 3, EK_HEADNORM = 4, EK_BIAS = 5 };
 
-// SiLU for the SwiGLU epilogue: hardware exp2 + reciprocal (≈2 ulp fp32 before the bf16 rounding
-// that follows; the reference's bf16 F.silu rounds the same value, model.py:118-122).
-__device__ __forceinline__ float silu_hw(float a) {
-  return a * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(a * -1.44269504088896341f));
-}
-
 // x from lane l ^ o (o = 8, 4, 2, 1: within 16-lane rows) without ds_bpermute's LDS round trip:
 // DPP row_ror:8 for 8 ((l + 8) mod 16 = l ^ 8), quad_perm for 2 and 1, ds_swizzle (bitmask mode,
 // xor 4) for 4 — the same lane pairs as __shfl_xor, so a butterfly sum is bitwise unchanged.
@@ -116,7 +110,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float a = rbf(acc[i][2 * jj][r]), b = rbf(acc[i][2 * jj + 1][r]);
-          u[r] = rbf(silu_hw(a)) * b;
+          u[r] = rbf(silu_bf16in(a)) * b;
         }
         const int c0 = jj * 16 + cq;
         const int ph = ((c0 >> 3) ^ (ml & (CH - 1))) * 8 + (c0 & 7);
@@ -1030,7 +1024,7 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float a = rbf(acc[ii][2 * jj][r]), b = rbf(acc[ii][2 * jj + 1][r]);
-            u[r] = rbf(silu_hw(a)) * b;
+            u[r] = rbf(silu_bf16in(a)) * b;
           }
           q[jj] = make_uint2(pack2bf(u[0], u[1]), pack2bf(u[2], u[3]));
         }

@@ -251,13 +251,18 @@ EchoAttnArgs attn_args(const Tensor& q, const optional<Tensor>& gate, at::Tensor
   need_dev(q, gate, "gate");
   EchoAttnArgs a{};
   a.dtype = dt_of(q, "q");
-  a.rows = i32(q.size(0), "rows");
+  // out rows may be a multiple of q's: output row r reads q / gate row r % q.size(0)
+  // (the identical CFG row groups of layer 0 share one q copy, EchoAttnArgs.q_batch_mod)
+  TORCH_CHECK(q.dim() == 4 && out.dim() == 4 && q.size(0) > 0 && out.size(0) % q.size(0) == 0 &&
+                  out.sizes().slice(1) == q.sizes().slice(1) && out.scalar_type() == q.scalar_type(),
+              "echo_hip.joint_attention: out must match q (rows: a multiple of q's)");
+  a.rows = i32(out.size(0), "rows");
+  a.q_batch_mod = out.size(0) == q.size(0) ? 0 : i32(q.size(0), "q rows");
   a.n_q = i32(q.size(1), "n_q");
   a.heads = i32(q.size(2), "heads");
   a.nseg = (int32_t)ns;
   a.q = q.data_ptr();
   std::tie(a.q_ld_tok, a.q_ld_batch) = head_view(q, "q");
-  TORCH_CHECK(out.sizes() == q.sizes() && out.scalar_type() == q.scalar_type(), "echo_hip.joint_attention: out must match q");
   a.out = out.data_ptr();
   std::tie(a.o_ld_tok, a.o_ld_batch) = head_view(out, "out");
   if (gate.has_value() && gate->defined()) {

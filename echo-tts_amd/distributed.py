@@ -40,13 +40,14 @@ def _world(group) -> Tuple[int, int]:
     return dist.get_world_size(group), dist.get_rank(group)
 
 
-def gather_rows(local: torch.Tensor, batch: int, group=None) -> torch.Tensor:
+def gather_rows(local: torch.Tensor, batch: int, group=None, force_collective: bool = False) -> torch.Tensor:
     """All-gather every rank's rows [stop_r - start_r, ...] into the global [batch, ...] on every rank.
 
     Shards are padded to ceil(batch / world) rows so a single fixed-size all-gather suffices
-    (RCCL `all_gather_into_tensor`; gloo, used by the CPU tests, gathers a list on the host)."""
+    (RCCL `all_gather_into_tensor`; gloo, used by the CPU tests, gathers a list on the host).
+    A single-rank group returns `local` unless force_collective (tests: the RCCL path on one GPU)."""
     world, rank = _world(group)
-    if world == 1:
+    if world == 1 and not (force_collective and dist.is_available() and dist.is_initialized()):
         return local
     rows = -(-batch // world)
     pad = local.new_zeros((rows,) + tuple(local.shape[1:]))
@@ -68,12 +69,20 @@ def gather_rows(local: torch.Tensor, batch: int, group=None) -> torch.Tensor:
 def sample_euler_cfg_sharded(model, speaker_latent: torch.Tensor, speaker_mask: torch.Tensor,
                              text_input_ids: torch.Tensor, text_mask: torch.Tensor, rng_seed: int, *,
                              group=None, gather: bool = True, sequence_length: Optional[int] = None,
-                             **sampler_kw) -> torch.Tensor:
+                             force_collective: bool = False, **sampler_kw) -> torch.Tensor:
     """`sample_euler_cfg_independent_guidances` over all ranks of `group`.
 
     Every rank passes the GLOBAL batch (ids, masks, speaker latents: a few MB) and the same seed;
     rank r samples prompts shard_range(B, G, r) with rows of the global x_T draw. Returns the
-    global [B, N, 80] latents on every rank (gather=True) or this rank's rows."""
+    global [B, N, 80] latents on every rank (gather=True) or this rank's rows.
+
+    Equality with one process sampling all B prompts: every kernel treats prompts independently,
+    except that the attention's split-KV count is chosen from the launch's row count
+    (`echo_attention_pick_split`: only launches with fewer (row, head, 128-query) items than half
+    the CUs split, e.g. 1 prompt per rank at 640 latents). Where a rank's launches pick the same
+    count as the one-process run (at 640 latents: >= 2 prompts per rank and the one-process batch
+    as well) the gathered batch is bitwise equal; otherwise it differs only in the fp32 summation
+    order over keys (fp32-close; bf16 outputs within the kernel's rounding)."""
     world, rank = _world(group)
     B = text_input_ids.shape[0]
     N = 640 if sequence_length is None else sequence_length
@@ -85,16 +94,18 @@ def sample_euler_cfg_sharded(model, speaker_latent: torch.Tensor, speaker_mask: 
                                 text_mask[s:e], noise[s:e], **sampler_kw)
     else:
         lat = noise[:0].clone()
-    return gather_rows(lat, B, group) if gather else lat
+    return gather_rows(lat, B, group, force_collective) if gather else lat
 
 
 @torch.inference_mode()
 def sample_blockwise_sharded(model, speaker_latent: torch.Tensor, speaker_mask: torch.Tensor,
                              text_input_ids: torch.Tensor, text_mask: torch.Tensor, rng_seed: int,
                              block_sizes: List[int], *, group=None, gather: bool = True,
-                             continuation_latent: Optional[torch.Tensor] = None, **sampler_kw) -> torch.Tensor:
+                             continuation_latent: Optional[torch.Tensor] = None, force_collective: bool = False,
+                             **sampler_kw) -> torch.Tensor:
     """`sample_blockwise_euler_cfg_independent_guidances` over all ranks of `group` (each block's
-    global x_T draw sliced to this rank's prompts)."""
+    global x_T draw sliced to this rank's prompts; equality with one process as in
+    `sample_euler_cfg_sharded`)."""
     world, rank = _world(group)
     B = text_input_ids.shape[0]
     s, e = shard_range(B, world, rank)
@@ -111,4 +122,4 @@ def sample_blockwise_sharded(model, speaker_latent: torch.Tensor, speaker_mask: 
     else:
         start0 = 0 if continuation_latent is None else continuation_latent.shape[1]
         lat = torch.empty((0, start0 + sum(block_sizes), 80), device=model.device)
-    return gather_rows(lat, B, group) if gather else lat
+    return gather_rows(lat, B, group, force_collective) if gather else lat

@@ -4,7 +4,7 @@ captured as a hipGraph (torch.cuda.CUDAGraph over the HIP stream).
 Everything data-dependent in the reference loop (inference.py:508-558) is
 resolved on the host BEFORE the loop, in fp32 CPU tensors exactly as the
 reference computes it (so no device->host sync remains inside the loop):
-  * t_i = linspace(1, 0, S+1)[i] * 0.999                      (inference.py:477)
+  * t_i = linspace(1, 0, S+1)[i] * 0.999 (device linspace)    (inference.py:477)
   * has_cfg_i = (t_i >= cfg_min_t) * (t_i <= cfg_max_t)        (inference.py:511)
   * dt_i = t_{i+1} - t_i, rescale coefficients                (inference.py:431-443,558)
   * the step at which the speaker-KV scale is undone           (inference.py:546-556)
@@ -41,26 +41,60 @@ class Schedule:
     unscale_step: Optional[int]     # step after which speaker KV is divided by its scale
 
 
+_SCHED_CACHE = {}
+
+
+def t_values(num_steps: int, device=None) -> torch.Tensor:
+    """t_schedule = linspace(1, 0, S+1) * 0.999 in fp32, computed on `device` exactly as the reference
+    does (`torch.linspace(..., device=model.device) * INIT_SCALE`, inference.py:477)."""
+    dev = torch.device("cpu") if device is None else torch.device(device)
+    return torch.linspace(1.0, 0.0, num_steps + 1, device=dev) * INIT_SCALE
+
+
 def make_schedule(num_steps: int, cfg_scale_text: float, cfg_scale_speaker: float, cfg_min_t: float,
                   cfg_max_t: float, rescale_k: Optional[float], rescale_sigma: Optional[float],
-                  speaker_kv_scale: Optional[float], speaker_kv_min_t: Optional[float]) -> Schedule:
-    ts = torch.linspace(1.0, 0.0, num_steps + 1) * INIT_SCALE
+                  speaker_kv_scale: Optional[float], speaker_kv_min_t: Optional[float], device=None) -> Schedule:
+    """The sampler's static schedule, evaluated once per argument set on `device` (the model's device
+    for the sampler; None = the host) with the reference's own expressions on its own device tensors:
+    t_i (inference.py:477), the CFG flag (:511), dt = t_{i+1} - t_i (:558), the rescale scalars
+    (:438-441: 1 - t, ratio, 1 / (1 - t)) and the speaker-KV un-scale step (:546-548). The reference
+    forms these per step on 0-dim device tensors; the same element-wise kernels over the [S] vector give
+    the same values (one device->host copy instead of a sync per step). Device and host can differ in
+    the last fp32 ulp (e.g. a device divides by a Python scalar as a reciprocal multiply, the host
+    divides): the sampler uses the device's values, as the reference on that device would."""
+    dev = torch.device("cpu") if device is None else torch.device(device)
+    key = (num_steps, cfg_scale_text, cfg_scale_speaker, cfg_min_t, cfg_max_t, rescale_k, rescale_sigma,
+           speaker_kv_scale, speaker_kv_min_t, str(dev))
+    if key in _SCHED_CACHE:
+        return _SCHED_CACHE[key]
+    ts = t_values(num_steps, dev)
+    t, tn = ts[:-1], ts[1:]
+    cols = [(t >= cfg_min_t) * (t <= cfg_max_t), tn - t]
+    resc = rescale_k is not None and rescale_sigma is not None
+    if resc:
+        snr = (1 - t) ** 2 / (t ** 2)
+        ratio = (snr * rescale_sigma ** 2 + 1) / (snr * rescale_sigma ** 2 / rescale_k + 1)
+        cols += [t < 1, 1 - t, ratio, 1 / (1 - t)]
+    if speaker_kv_scale is not None:
+        cols.append((tn < speaker_kv_min_t) * (t >= speaker_kv_min_t))
+    host = [c.cpu() for c in cols]
+    tsh = ts.cpu()
     has_cfg, args = [], []
     unscale = None
     for i in range(num_steps):
-        t, tn = ts[i], ts[i + 1]
-        cfg = bool(((t >= cfg_min_t) * (t <= cfg_max_t)).item())
-        dt = float(tn - t)
-        resc, omt, ratio, inv = 0, 0.0, 0.0, 0.0
-        if rescale_k is not None and rescale_sigma is not None and bool(t < 1):
-            snr = (1 - t) ** 2 / (t ** 2)
-            r = (snr * rescale_sigma ** 2 + 1) / (snr * rescale_sigma ** 2 / rescale_k + 1)
-            resc, omt, ratio, inv = 1, float(1 - t), float(r), float(1 / (1 - t))
+        cfg = bool(host[0][i])
+        dt = float(host[1][i])
+        r = (1, float(host[3][i]), float(host[4][i]), float(host[5][i])) if resc and bool(host[2][i]) else \
+            (0, 0.0, 0.0, 0.0)
         has_cfg.append(cfg)
-        args.append((int(cfg), float(cfg_scale_text), float(cfg_scale_speaker), resc, omt, ratio, inv, dt))
-        if speaker_kv_scale is not None and bool(tn < speaker_kv_min_t) and bool(t >= speaker_kv_min_t):
+        args.append((int(cfg), float(cfg_scale_text), float(cfg_scale_speaker)) + r + (dt,))
+        if speaker_kv_scale is not None and bool(host[-1][i]):
             unscale = i  # the reference's condition can only hold once on a decreasing schedule
-    return Schedule(num_steps, tuple(float(v) for v in ts), tuple(has_cfg), tuple(args), unscale)
+    sched = Schedule(num_steps, tuple(float(v) for v in tsh), tuple(has_cfg), tuple(args), unscale)
+    if len(_SCHED_CACHE) > 64:
+        _SCHED_CACHE.clear()
+    _SCHED_CACHE[key] = sched
+    return sched
 
 
 def step_args(fields: Tuple) -> L.StepArgs:
@@ -366,7 +400,34 @@ class StreamSplit:
                     p.run(True)
             for st in self.streams:
                 cur.wait_stream(st)
+        return self.output()
+
+    def output(self) -> torch.Tensor:
         return torch.cat([p.output() for p in self.parts])
+
+    @property
+    def graph(self):
+        """The parts' captured graphs (None until every part has captured)."""
+        gs = tuple(p.graph for p in self.parts)
+        return None if any(g is None for g in gs) else gs
+
+    @torch.no_grad()
+    def nfe(self, *args) -> torch.Tensor:
+        """Teacher-forced model output with the parts' buffers (the surface of CFGPlan.nfe(i, x) /
+        BlockPlan.nfe(b, i, x, prefix)): the state is split by prompt, and the parts' outputs
+        [copies * b_part, N, 80] are re-assembled into the one-plan layout [copies * B, N, 80]
+        (CFG row groups [cond | uncond-text | uncond-speaker], each over all B prompts)."""
+        outs = []
+        for p, (a, b) in zip(self.parts, self.bounds):
+            if isinstance(p, BlockPlan):
+                blk, i, x, prefix = args
+                outs.append(p.nfe(blk, i, x[a:b], prefix[a:b]))
+            else:
+                i, x = args
+                outs.append(p.nfe(i, x[a:b]))
+        copies = outs[0].shape[0] // self.parts[0].B
+        return torch.cat([o.view(copies, p.B, *o.shape[1:]) for o, p in zip(outs, self.parts)], 1) \
+            .view(copies * self.B, *outs[0].shape[1:])
 
 
 _single_stream = [False]
@@ -406,7 +467,9 @@ def _cached(model: EchoDiTHip, key, make):
 def get_plan(model: EchoDiTHip, B: int, N: int, Tc: int, Pc: int, sched: Schedule,
              kv_scale: Optional[float], kv_max_layers: Optional[int]):
     """The plan for one sampler shape: a `CFGPlan`, or a two-stream `StreamSplit` of two half-batch
-    CFGPlans for B x N >= STREAM_SPLIT_MIN_TOKENS (same setup/run surface)."""
+    CFGPlans for B x N >= STREAM_SPLIT_MIN_TOKENS. Both offer setup / run / output / nfe / graph
+    (StreamSplit.graph is the parts' graphs; its `x`, `ws` and buffers live in its `parts`); callers
+    that need one CFGPlan's buffers make the plan inside `single_stream()`."""
     sizes = _split_sizes(B, N)
     if sizes is None:
         return _cached(model, plan_key(B, N, Tc, Pc, sched, kv_scale, kv_max_layers),

@@ -301,7 +301,7 @@ def sample_with_noise(model, speaker_latent, speaker_mask, text_input_ids, text_
                              rescale_k, rescale_sigma, speaker_kv_scale, speaker_kv_max_layers, speaker_kv_min_t)
     B, N = noise.shape[0], noise.shape[1]
     sched = E.make_schedule(num_steps, cfg_scale_text, cfg_scale_speaker, cfg_min_t, cfg_max_t, rescale_k,
-                            rescale_sigma, speaker_kv_scale, speaker_kv_min_t)
+                            rescale_sigma, speaker_kv_scale, speaker_kv_min_t, device=model.device)
     Tc, Pc = E.caps(model, text_input_ids, text_mask, speaker_latent, speaker_mask)
     plan = E.get_plan(model, B, N, Tc, Pc, sched, speaker_kv_scale, speaker_kv_max_layers)
     plan.setup(text_input_ids, text_mask, speaker_latent, speaker_mask, noise.to(model.device, torch.float32),

@@ -59,7 +59,7 @@ def blockwise_with_noise(model, speaker_latent, speaker_mask, text_input_ids, te
                                   truncation_factor, rescale_k, rescale_sigma, speaker_kv_scale,
                                   speaker_kv_max_layers, speaker_kv_min_t, continuation_latent)
     sched = E.make_schedule(num_steps, cfg_scale_text, cfg_scale_speaker, cfg_min_t, cfg_max_t, rescale_k,
-                            rescale_sigma, speaker_kv_scale, speaker_kv_min_t)
+                            rescale_sigma, speaker_kv_scale, speaker_kv_min_t, device=model.device)
     B = text_input_ids.shape[0]
     Tc, Pc = E.caps(model, text_input_ids, text_mask, speaker_latent, speaker_mask)
     start0 = 0 if continuation_latent is None else continuation_latent.shape[1]

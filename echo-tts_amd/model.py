@@ -236,27 +236,38 @@ class EchoDiTHip:
 
     # ------------------------------------------------------------------ encoders
     def _encoder(self, enc: Encoder, x: Tensor, B: int, Lq: int, lens: Optional[List[int]], causal: bool) -> Tensor:
-        """EncoderTransformerBlock stack (model.py:335-339) in place on x [B*Lq, Dm]."""
-        eps = self.cfg.norm_eps
+        """EncoderTransformerBlock stack (model.py:335-339, 420-423, 458-466) in place on x [B*Lq, Dm]."""
+        scratch = self._encoder_scratch(enc, x, lens)
+        for i in range(len(enc.layers)):
+            self.encoder_layer(enc, i, x, B, Lq, lens, causal, scratch)
+        return x
+
+    @staticmethod
+    def _encoder_scratch(enc: Encoder, x: Tensor, lens: Optional[List[int]]):
         M, Dm = x.shape
-        h = enc.heads
-        xn = torch.empty_like(x)
-        qkvg = torch.empty((M, 4 * Dm), device=x.device, dtype=x.dtype)
-        og = torch.empty_like(x)
-        u = torch.empty((M, enc.ffn), device=x.device, dtype=x.dtype)
         lens_d = None if lens is None else torch.tensor(lens, dtype=torch.int32).to(x.device)
+        return (torch.empty_like(x), torch.empty((M, 4 * Dm), device=x.device, dtype=x.dtype), torch.empty_like(x),
+                torch.empty((M, enc.ffn), device=x.device, dtype=x.dtype), lens_d)
+
+    def encoder_layer(self, enc: Encoder, i: int, x: Tensor, B: int, Lq: int, lens: Optional[List[int]],
+                      causal: bool, scratch=None) -> Tensor:
+        """EncoderTransformerBlock.forward (model.py:335-339) of layer i in place on x [B*Lq, Dm]:
+        x += Attn(RMSNorm(x)) (full RoPE; key-padding `lens` or causal); x += MLP(RMSNorm(x))."""
+        eps = self.cfg.norm_eps
+        h = enc.heads
+        lay = enc.layers[i]
+        xn, qkvg, og, u, lens_d = scratch if scratch is not None else self._encoder_scratch(enc, x, lens)
         v4 = qkvg.view(B, Lq, 4, h, 128)
-        for lay in enc.layers:
-            ops.rmsnorm(x, lay.attn_norm, eps, out=xn)
-            ops.gemm(xn, lay.wqkvg, out=qkvg,
-                     head_norm=ops.HeadNorm(lay.qk_norm, h, 2, eps, w_stride=h * 128, rope=self.rope,
-                                            rope_heads=h, seq_len=Lq))
-            ops.attention(v4[:, :, 0], [ops.Segment(v4[:, :, 1], v4[:, :, 2], lens=lens_d, causal=causal)],
-                          out=og.view(B, Lq, h, 128), gate=v4[:, :, 3])
-            ops.gemm(og, lay.wo, out=x, epilogue=L.EPI_RESID, aux=x)
-            ops.rmsnorm(x, lay.mlp_norm, eps, out=xn)
-            ops.gemm(xn, lay.w13, out=u, epilogue=L.EPI_SWIGLU)
-            ops.gemm(u, lay.w2, out=x, epilogue=L.EPI_RESID, aux=x)
+        ops.rmsnorm(x, lay.attn_norm, eps, out=xn)
+        ops.gemm(xn, lay.wqkvg, out=qkvg,
+                 head_norm=ops.HeadNorm(lay.qk_norm, h, 2, eps, w_stride=h * 128, rope=self.rope,
+                                        rope_heads=h, seq_len=Lq))
+        ops.attention(v4[:, :, 0], [ops.Segment(v4[:, :, 1], v4[:, :, 2], lens=lens_d, causal=causal)],
+                      out=og.view(B, Lq, h, 128), gate=v4[:, :, 3])
+        ops.gemm(og, lay.wo, out=x, epilogue=L.EPI_RESID, aux=x)
+        ops.rmsnorm(x, lay.mlp_norm, eps, out=xn)
+        ops.gemm(xn, lay.w13, out=u, epilogue=L.EPI_SWIGLU)
+        ops.gemm(u, lay.w2, out=x, epilogue=L.EPI_RESID, aux=x)
         return x
 
     def _kv_project(self, st: Tensor, w_kv: Tensor, B: int, Tc: int, latent_rope: bool,
@@ -386,64 +397,66 @@ class EchoDiTHip:
         segs: [latent, text, speaker] segments (None = absent) shared by all layers, or a
         callable layer -> such a list; self-attention keys come from ws.qkvg.
         copies: the rows are `copies` identical groups of R / copies (the CFG batch, inference.py:516:
-        the same x three times). Layer 0's AdaLN and QKVG projection then run on one group only —
-        its Q/K/V/gate are the same for every group — and its attention runs once per group with
-        that group's text/speaker lengths (bitwise equal to the full computation).
+        the same x three times); see `decoder_layer(share_copies=...)` for what layer 0 does with that.
         """
-        cfg = self.cfg
-        D, H, eps = cfg.model_size, cfg.num_heads, cfg.norm_eps
         if start_pos + N > MAX_POS:
             raise ValueError("sequence exceeds the RoPE table")
         M = R * N
         ops.gemm(ws.xin, self.w_in, out=ws.h, bias=self.b_in)
-        q4 = ws.qkvg.view(R, N, 4, H, 128)
-        self_seg = ops.Segment(q4[:, :, 1], q4[:, :, 2])
-        og4 = ws.og.view(R, N, H, 128)
-        shared = None if callable(segs) else [self_seg] + [s for s in segs if s is not None]
         share0 = copies > 1 and not per_row_tab and SHARE_LAYER0 and R % copies == 0
-        Rg = R // copies if share0 else R
-        for i, lay in enumerate(self.layers):
-            all_segs = shared if shared is not None else [self_seg] + [s for s in segs(i) if s is not None]
-            for a in range(2):
-                if per_row_tab:
-                    sh, s1, g = tab[:, 2 * i + a, 0], tab[:, 2 * i + a, 1], tab[:, 2 * i + a, 2]
-                else:
-                    sh, s1, g = tab[2 * i + a, 0], tab[2 * i + a, 1], tab[2 * i + a, 2]
-                if a == 0 and i == 0 and share0:
-                    # layer 0 of identical row groups: AdaLN + QKVG on the first group only
-                    Mg = Rg * N
-                    ops.adaln_modulate(ws.h[:Mg], sh, s1, eps, ws.xn[:Mg])
-                    ops.gemm(ws.xn[:Mg], lay.wqkvg, out=ws.qkvg[:Mg],
-                             head_norm=ops.HeadNorm(lay.qk_norm, H, 2, eps, w_stride=H * 128, rope=self.rope,
-                                                    rope_heads=H // 2, seq_len=N, pos0=start_pos))
-                    qg = ws.qkvg[:Mg].view(Rg, N, 4, H, 128)
-                    for c in range(copies):
-                        gs = [ops.Segment(qg[:, :, 1], qg[:, :, 2])]
-                        for sg in all_segs[1:]:
-                            gs.append(ops.Segment(sg.k, sg.v, None if sg.lens is None else sg.lens[c * Rg:(c + 1) * Rg],
-                                                  sg.batch_mod, sg.causal))
-                        ops.attention(qg[:, :, 0], gs, out=og4[c * Rg:(c + 1) * Rg], gate=qg[:, :, 3])
-                    src, w = ws.og, lay.wo
-                elif a == 0:
-                    ops.adaln_modulate(ws.h, sh, s1, eps, ws.xn)
-                    # QKVG projection with q/k RMSNorm + half RoPE fused into its epilogue
-                    ops.gemm(ws.xn, lay.wqkvg, out=ws.qkvg,
-                             head_norm=ops.HeadNorm(lay.qk_norm, H, 2, eps, w_stride=H * 128, rope=self.rope,
-                                                    rope_heads=H // 2, seq_len=N, pos0=start_pos))
-                    ops.attention(q4[:, :, 0], all_segs, out=og4, gate=q4[:, :, 3])
-                    src, w = ws.og, lay.wo
-                else:
-                    ops.adaln_modulate(ws.h, sh, s1, eps, ws.xn)
-                    ops.gemm(ws.xn, lay.w13, out=ws.u, epilogue=L.EPI_SWIGLU)
-                    src, w = ws.u, lay.w2
-                if per_row_tab:
-                    h3 = ws.h.view(R, N, D)
-                    ops.gemm(src.view(R, N, -1), w, out=h3, epilogue=L.EPI_RESID, aux=h3, gate=g)
-                else:
-                    ops.gemm(src, w, out=ws.h, epilogue=L.EPI_RESID, aux=ws.h, gate=g)
+        for i in range(len(self.layers)):
+            self.decoder_layer(ws, i, R, N, tab, segs if not callable(segs) else segs(i), start_pos, per_row_tab,
+                               share_copies=copies if (i == 0 and share0) else 1)
+        eps = self.cfg.norm_eps
         ops.rmsnorm(ws.h, self.out_norm, eps, out=ws.xn)
         ops.gemm(ws.xn, self.w_out, out=ws.v, bias=self.b_out, epilogue=L.EPI_F32OUT)
         return ws.v[:M]
+
+    def decoder_layer(self, ws: Workspace, i: int, R: int, N: int, tab: Tensor, segs: Sequence,
+                      start_pos: int = 0, per_row_tab: bool = False, share_copies: int = 1) -> None:
+        """TransformerBlock.forward (model.py:371-390) of layer i, in place on ws.h [R*N, D] (bf16
+        residual stream): x += g_a * Attn(AdaLN_a(x)); x += g_m * MLP(AdaLN_m(x)).
+
+        tab: the whole [2L, 3, D] table (or [R, 2L, 3, D] with per_row_tab); segs: this layer's
+        [latent, text, speaker] conditioning segments (None = absent).
+        share_copies > 1: ws.h holds share_copies identical row groups (layer 0 of a CFG step,
+        inference.py:516). The AdaLN and the QKVG projection (q/k norm + RoPE) then run on the first
+        group only — its q/k/v/gate are those of every group — and ONE attention launch over all R
+        rows reads that group's q/gate/self K/V for every row (q row r % Rg, `EchoAttnArgs.q_batch_mod`)
+        with each row's own text/speaker lengths: the same launch shape, split-KV choice and per-row
+        arithmetic as the unshared layer, so the result is bitwise equal."""
+        cfg = self.cfg
+        D, H, eps = cfg.model_size, cfg.num_heads, cfg.norm_eps
+        lay = self.layers[i]
+        Rg = R // share_copies
+        q4 = ws.qkvg.view(R, N, 4, H, 128)
+        og4 = ws.og.view(R, N, H, 128)
+        cond_segs = [s for s in segs if s is not None]
+        for a in range(2):
+            if per_row_tab:
+                sh, s1, g = tab[:, 2 * i + a, 0], tab[:, 2 * i + a, 1], tab[:, 2 * i + a, 2]
+            else:
+                sh, s1, g = tab[2 * i + a, 0], tab[2 * i + a, 1], tab[2 * i + a, 2]
+            if a == 0:
+                Mg = Rg * N
+                ops.adaln_modulate(ws.h[:Mg], sh, s1, eps, ws.xn[:Mg])
+                # QKVG projection with q/k RMSNorm + half RoPE fused into its epilogue
+                ops.gemm(ws.xn[:Mg], lay.wqkvg, out=ws.qkvg[:Mg],
+                         head_norm=ops.HeadNorm(lay.qk_norm, H, 2, eps, w_stride=H * 128, rope=self.rope,
+                                                rope_heads=H // 2, seq_len=N, pos0=start_pos))
+                qg = ws.qkvg[:Mg].view(Rg, N, 4, H, 128) if share_copies > 1 else q4
+                self_seg = ops.Segment(qg[:, :, 1], qg[:, :, 2], batch_mod=Rg)
+                ops.attention(qg[:, :, 0], [self_seg] + cond_segs, out=og4, gate=qg[:, :, 3])
+                src, w = ws.og, lay.wo
+            else:
+                ops.adaln_modulate(ws.h, sh, s1, eps, ws.xn)
+                ops.gemm(ws.xn, lay.w13, out=ws.u, epilogue=L.EPI_SWIGLU)
+                src, w = ws.u, lay.w2
+            if per_row_tab:
+                h3 = ws.h.view(R, N, D)
+                ops.gemm(src.view(R, N, -1), w, out=h3, epilogue=L.EPI_RESID, aux=h3, gate=g)
+            else:
+                ops.gemm(src, w, out=ws.h, epilogue=L.EPI_RESID, aux=ws.h, gate=g)
 
     # ------------------------------------------------------------------ generic forward (API)
     @torch.no_grad()

@@ -152,7 +152,8 @@ class AttnTimer:
             e0.record(s)
             r = timer._orig(q, segments, out=out, gate=gate, scale=scale)
             e1.record(s)
-            R, nq, H = q.shape[0], q.shape[1], q.shape[2]
+            # rows = the output's (q may hold fewer rows, broadcast to the output by q_batch_mod)
+            R, nq, H = (out if out is not None else q).shape[0], q.shape[1], q.shape[2]
             segs = [(sg.k.shape[1], None if sg.lens is None else sg.lens.clone(), bool(sg.causal)) for sg in segments]
             timer.records.append((e0, e1, R, nq, H, segs))
             return r

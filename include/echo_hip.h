@@ -116,6 +116,8 @@ typedef struct {
   void* out; int64_t o_ld_tok, o_ld_batch;
   float scale;              /* softmax scale, 1/sqrt(128) */
   EchoKVSegment seg[4];     /* [self | latent | text | speaker] */
+  int32_t q_batch_mod;      /* q and gate of output row r are row r % q_batch_mod (0 = row r): the CFG
+                               batch's identical layer-0 row groups (inference.py:516) read one copy */
 } EchoAttnArgs;
 
 /* Replaces the KV concat + F.scaled_dot_product_attention + sigmoid gate of

@@ -48,7 +48,7 @@ def _worker(rank, world, port, batch, q):
     lat = noise + spk[s:e, :4, :] + ids[s:e, :4, None].float()
     out = D.gather_rows(lat, batch)
     t = bench.max_over_ranks(dist, 1.0 + rank, torch.device("cpu"))
-    q.put((rank, out, t))
+    q.put((rank, out.numpy(), t))  # by value (a shared-fd tensor dies with an exited worker)
     dist.destroy_process_group()
 
 
@@ -63,7 +63,7 @@ def test_shards_and_gather(world, batch):
     res = {}
     for _ in range(world):
         r, out, t = q.get(timeout=120)
-        res[r] = (out, t)
+        res[r] = (torch.from_numpy(out), t)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

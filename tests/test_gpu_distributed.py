@@ -64,7 +64,9 @@ def _worker(rank, world, port, q, split=False):
     ids, tm, spk, sm = _inputs()
     lat = D.sample_euler_cfg_sharded(m, spk, sm, ids, tm, 11, sequence_length=N, **KW).cpu()
     blk = D.sample_blockwise_sharded(m, spk, sm, ids, tm, 12, BLOCKS, **KW_BLK).cpu()
-    q.put((rank, lat, blk))
+    # numpy arrays travel by value: torch CPU tensors would be shared through a file descriptor that
+    # dies with this process if it exits before the parent has received them
+    q.put((rank, lat.numpy(), blk.numpy()))
     dist.destroy_process_group()
 
 
@@ -79,7 +81,7 @@ def test_two_rank_sharded_samplers_match_single_process(split):
     res = {}
     for _ in range(world):
         r, lat, blk = q.get(timeout=110)
-        res[r] = (lat, blk)
+        res[r] = (torch.from_numpy(lat), torch.from_numpy(blk))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -93,3 +95,43 @@ def test_two_rank_sharded_samplers_match_single_process(split):
     assert torch.isfinite(full).all() and torch.isfinite(full_blk).all()
     assert torch.equal(res[0][0], full), float((res[0][0] - full).abs().max())
     assert torch.equal(res[0][1], full_blk), float((res[0][1] - full_blk).abs().max())
+
+
+def _rccl_worker(port, q):
+    """A single-rank RCCL ('nccl') group: gather_rows' all_gather_into_tensor path runs for real
+    (force_collective skips the world-size-1 shortcut)."""
+    import sys
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    from echo_tts_amd import distributed as D
+    m = _model()
+    ids, tm, spk, sm = _inputs()
+    lat = D.sample_euler_cfg_sharded(m, spk, sm, ids, tm, 11, sequence_length=N, force_collective=True, **KW)
+    blk = D.sample_blockwise_sharded(m, spk, sm, ids, tm, 12, BLOCKS, force_collective=True, **KW_BLK)
+    # the padded gather itself: rows of an odd-sized shard land in order, device-resident
+    x = torch.arange(5 * 7, dtype=torch.float32, device="cuda:0").view(5, 7)
+    g = D.gather_rows(x, 5, force_collective=True)
+    q.put((lat.cpu().numpy(), blk.cpu().numpy(), g.device.type, torch.equal(g.cpu(), x.cpu())))
+    dist.destroy_process_group()
+
+
+def test_rccl_gather_single_rank_matches_unsharded():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    lat, blk, gdev, g_ok = q.get(timeout=110)
+    lat, blk = torch.from_numpy(lat), torch.from_numpy(blk)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert gdev == "cuda" and g_ok
+    from echo_tts_amd.inference import sample_euler_cfg_independent_guidances
+    from echo_tts_amd.inference_blockwise import sample_blockwise_euler_cfg_independent_guidances
+    m = _model()
+    ids, tm, spk, sm = _inputs()
+    full = sample_euler_cfg_independent_guidances(m, spk, sm, ids, tm, 11, sequence_length=N, **KW).cpu()
+    full_blk = sample_blockwise_euler_cfg_independent_guidances(m, spk, sm, ids, tm, 12, BLOCKS, **KW_BLK).cpu()
+    assert torch.equal(lat, full) and torch.equal(blk, full_blk)

@@ -81,7 +81,7 @@ def test_c2_engine_teacher_forced_bf16(m16, c2):
     spk, sm, ids, tm = _inputs(g)
     kw = _kw(meta)
     sched = En.make_schedule(kw["num_steps"], kw["cfg_scale_text"], kw["cfg_scale_speaker"], kw["cfg_min_t"],
-                             kw["cfg_max_t"], None, None, None, None)
+                             kw["cfg_max_t"], None, None, None, None, device=DEV)
     Tc, Pc = En.caps(m16, ids, tm, spk, sm)
     assert (Tc, Pc) == (448, 160)  # the production trimming
     plan = En.get_plan(m16, 1, 640, Tc, Pc, sched, None, None)
@@ -132,7 +132,7 @@ def test_c3_rows_bitwise_equal_b1(m16, c2):
 def _block_plan(m, g, meta, B=1):
     kw = _kw(meta)
     sched = En.make_schedule(kw["num_steps"], kw["cfg_scale_text"], kw["cfg_scale_speaker"], kw["cfg_min_t"],
-                             kw["cfg_max_t"], None, None, kw["speaker_kv_scale"], kw["speaker_kv_min_t"])
+                             kw["cfg_max_t"], None, None, kw["speaker_kv_scale"], kw["speaker_kv_min_t"], device=DEV)
     spk, sm, ids, tm = _inputs(g)
     Tc, Pc = En.caps(m, ids, tm, spk, sm)
     plan = En.get_block_plan(m, B, meta["blocks"], 0, Tc, Pc, sched, kw["speaker_kv_scale"],
@@ -189,7 +189,7 @@ def test_c5_engine_end_to_end_bf16(m16, c5):
 def _cont_plan(m, g, meta):
     kw = _kw(meta)
     sched = En.make_schedule(kw["num_steps"], kw["cfg_scale_text"], kw["cfg_scale_speaker"], kw["cfg_min_t"],
-                             kw["cfg_max_t"], kw["rescale_k"], kw["rescale_sigma"], None, None)
+                             kw["cfg_max_t"], kw["rescale_k"], kw["rescale_sigma"], None, None, device=DEV)
     spk, sm, ids, tm = _inputs(g)
     Tc, Pc = En.caps(m, ids, tm, spk, sm)
     plan = En.get_block_plan(m, 1, meta["blocks"], meta["prefix"], Tc, Pc, sched, None, None)

@@ -701,6 +701,28 @@ def test_euler_step_matches_reference_expression():
     assert torch.equal(x.cpu(), ref), float((x.cpu() - ref).abs().max())
 
 
+def test_schedule_is_the_device_linspace():
+    """t_i exactly as the reference forms them on the model's device — torch.linspace(1, 0, S+1,
+    device=device) * 0.999 (inference.py:477) — and the per-step scalars (CFG flag :511, rescale
+    :431-443, dt :558) equal to the reference's 0-dim device-tensor arithmetic, bitwise."""
+    from echo_tts_amd import engine as En
+    for S in (4, 10, 40, 64):
+        ts = torch.linspace(1.0, 0.0, S + 1, device=DEV) * 0.999
+        sched = En.make_schedule(S, 3.0, 8.0, 0.5, 1.0, 1.2, 3.0, 1.5, 0.9, device=DEV)
+        assert torch.equal(torch.tensor(sched.t, dtype=torch.float32), ts.cpu())
+        host = torch.linspace(1.0, 0.0, S + 1) * 0.999
+        print(f"S={S}: {int((host != ts.cpu()).sum())} of {S + 1} host-linspace t values differ from the device's")
+        for i in range(S):
+            t, tn = ts[i], ts[i + 1]
+            assert sched.has_cfg[i] == bool(((t >= 0.5) * (t <= 1.0)).item())
+            a = sched.args[i]
+            assert a[7] == float(tn - t)
+            if bool(t < 1):
+                snr = (1 - t) ** 2 / (t ** 2)
+                ratio = (snr * 3.0 ** 2 + 1) / (snr * 3.0 ** 2 / 1.2 + 1)
+                assert (a[4], a[5], a[6]) == (float(1 - t), float(ratio), float(1 / (1 - t)))
+
+
 def test_small_ops():
     ids = torch.randint(0, 256, (3, 17), dtype=torch.int32, device=DEV)
     tab = torch.randn(256, 128, device=DEV).to(BF)
