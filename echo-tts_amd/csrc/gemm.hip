@@ -818,11 +818,16 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
                     const bf16_t* __restrict__ W, int64_t ldw, int64_t sW,
                     void* __restrict__ Cv, int64_t ldc, int64_t sC,
                     int M, int N, int K, int tiles_m, int tiles_n, Epi ep) {
-  static_assert(EK == EK_STORE || EK == EK_SWIGLU || EK == EK_RESID || EK == EK_BIAS, "register epilogue kinds");
+  static_assert(EK == EK_STORE || EK == EK_SWIGLU || EK == EK_RESID || EK == EK_BIAS || EK == EK_HEADNORM,
+                "register epilogue kinds");
   constexpr int BM = 256, BN = 256, TM = 128, TN = 64, FM = 8, FN = 4;
   constexpr int STAGE = (BM + BN) * BK;
   constexpr int SN = reg_epi_stores(EK);
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+  // HEADNORM: per-(row, 8-column chunk) sums of squares of every wave, read by the partner wave that
+  // holds the other 64 columns of the head (8 waves x 128 rows x 8 chunks fp32 = 32 KB; with the
+  // 128 KB double buffer the workgroup declares all 160 KB of the CU's LDS)
+  __shared__ float hnx[EK == EK_HEADNORM ? 8 * TM * 8 : 1];
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -999,6 +1004,27 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
         for (int p = 0; p < FN / 2; ++p) load8(gp + p * 32, g[p]);
       }
     }
+    // HEADNORM (q/k RMSNorm + half RoPE, ECHO_EPI_HEADNORM): the head of this wave's 64 columns (a head is
+    // the 128 columns of waves (wm, 2p) and (wm, 2p+1)), its flags, and the norm weights of this lane's 16
+    // columns, loaded before the prologue DMA like RESID's residual rows
+    const int hidx = (n0 + (wn & ~1) * TN) >> 7;
+    const int hblk = EK == EK_HEADNORM ? hidx / ep.hn_heads : 0;
+    const int hhd = hidx - hblk * (EK == EK_HEADNORM ? ep.hn_heads : 0);
+    const bool hnorm = EK == EK_HEADNORM && hblk < ep.hn_nblk;
+    const bool hrope = hnorm && hhd < ep.hn_rope_heads;
+    // lane-derived values recomputed from an opaque copy of the lane id, so that the compiler does not
+    // hoist them above the K loop (which runs at the 256-VGPR limit)
+    int hl = lane;
+    if constexpr (EK == EK_HEADNORM) asm volatile("" : "+v"(hl));
+    const int hg = hl >> 4, hrow = hl & 15;
+    uint2 hw[FN];  // norm weights of this lane's 16 columns, loaded before the prologue DMA
+    if constexpr (EK == EK_HEADNORM) {
+      if (hnorm) {
+        const bf16_t* wp = (const bf16_t*)ep.hn_w + hblk * ep.hn_w_stride + hhd * 128 + (wn & 1) * TN + 4 * hg;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) hw[j] = *(const uint2*)(wp + j * 16);
+      }
+    }
     int m0n = 0, n0n = 0;
     if (more) {
       origin(tnext, m0n, n0n);
@@ -1011,7 +1037,126 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
     }
 
     // ---- epilogue from registers: exactly SN buffer stores per wave
-    if constexpr (EK == EK_SWIGLU) {
+    if constexpr (EK == EK_HEADNORM) {
+      // Bitwise equal to gemm_epilogue's HEADNORM kind (and to echo_head_norm_rope): v = bf16(acc) (the
+      // store rounding); per 8-column chunk c of a head the sum of squares in column order from 0; then
+      // the 16-lane butterfly's tree over chunks (c ^ 8, c ^ 4, c ^ 2, c ^ 1; every level adds the same
+      // two operands in either lane, so all chunks end with the same value); r = 1 / sqrtf(ss / 128 + eps);
+      // v = bf16(v * r * w); RoPE on column pairs in fp32; one rounding at the store.
+      // Register layout: acc[i][j][e] = row wm*128 + i*16 + (lane & 15), column wn*64 + j*16 + 4g + e
+      // (g = lane >> 4): chunk 2j + (g >> 1) of the wave's 8, its columns 0-3 in lanes g = 0, 2 and 4-7 in
+      // lanes g = 1, 3 (the partial sum crosses lane ^ 16 once); chunk c ^ 8 is the partner wave's same
+      // chunk (LDS), c ^ 4 and c ^ 2 are this lane's j ^ 2 and j ^ 1, c ^ 1 is lane ^ 32.
+      const int g = hg;
+      const bool hi16 = (g & 1) != 0;
+      uint2 hp[FM][FN];   // the store rounding first: bf16(acc), 2 per register (acc is dead after this)
+#pragma unroll
+      for (int ii = 0; ii < FM; ++ii)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          hp[ii][j] = make_uint2(pack2bf(acc[ii][j][0], acc[ii][j][1]), pack2bf(acc[ii][j][2], acc[ii][j][3]));
+      auto unpack = [](uint2 u, float (&v)[4]) __attribute__((always_inline)) {
+        v[0] = bf2f(u.x & 0xffffu); v[1] = bf2f(u.x >> 16); v[2] = bf2f(u.y & 0xffffu); v[3] = bf2f(u.y >> 16);
+      };
+      // (cos, sin) of this lane's 2 column pairs per j (fp32 table rows, like the reference's complex64
+      // freqs, model.py:9-24), 4 rows at a time (64 registers), loaded after the prologue DMA (issuing
+      // them before it, or before the sums below, spills: the K loop runs at 256 VGPRs)
+      float4 rc[FM / 2][FN];
+      auto load_rope = [&](int i0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int ii = 0; ii < FM / 2; ++ii) {
+          const int m = m0 + wm * TM + (i0 + ii) * 16 + hrow;
+          const int pos = ep.hn_pos0 + ep.hn_pos_mult * (min(m, M - 1) % ep.hn_seq_len);
+          const float* rp = ep.hn_rope + ((int64_t)pos * 64 + (wn & 1) * 32 + 2 * g) * 2;
+#pragma unroll
+          for (int j = 0; j < FN; ++j) rc[ii][j] = *(const float4*)(rp + j * 16);
+        }
+      };
+      if (hnorm) {
+#pragma unroll
+        for (int ii = 0; ii < FM; ++ii)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            float v[4];
+            unpack(hp[ii][j], v);
+            float h = 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) h += v[e] * v[e];   // columns 0-3 (lanes g = 0, 2)
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(h), __float_as_uint(h), false, false);
+            float c8 = __uint_as_float(hi16 ? sw[0] : sw[1]);   // lane ^ 16's partial
+#pragma unroll
+            for (int e = 0; e < 4; ++e) c8 += v[e] * v[e];  // columns 4-7 continue it: the chunk's sum
+            if (hi16) hnx[(wid * TM + ii * 16 + hrow) * 8 + 2 * j + (g >> 1)] = c8;
+          }
+      }
+      // every wave (all take this path) has written its chunk sums: raw barrier after the LDS writes retire
+      // (__syncthreads' fence would also wait for the prologue DMA, vmcnt(0))
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      pp_barrier();
+      if (hnorm) {
+        float hr[FM];
+#pragma unroll
+        for (int ii = 0; ii < FM; ++ii) {
+          float t1[FN];
+          const int ro = ii * 16 + hrow;
+#pragma unroll
+          for (int j = 0; j < FN; ++j)   // lanes g = 1, 3: this chunk + the partner wave's same chunk (c ^ 8)
+            t1[j] = hnx[(wid * TM + ro) * 8 + 2 * j + (g >> 1)] + hnx[((wid ^ 1) * TM + ro) * 8 + 2 * j + (g >> 1)];
+          const float t3 = (t1[0] + t1[2]) + (t1[1] + t1[3]);   // c ^ 4 (j ^ 2), then c ^ 2 (j ^ 1)
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(t3), __float_as_uint(t3), false, false);
+          const float t4 = t3 + __uint_as_float(hl >= 32 ? sw[0] : sw[1]);   // c ^ 1 (lane ^ 32)
+          const float r = 1.0f / sqrtf(t4 / 128.0f + ep.hn_eps);
+          const auto sr = __builtin_amdgcn_permlane16_swap(__float_as_uint(r), __float_as_uint(r), false, false);
+          hr[ii] = hi16 ? r : __uint_as_float(sr[1]);  // lanes g = 0, 2 take lane ^ 16's
+        }
+        if (more) vm_wait_n<14>(); else vm_wait_n<0>();   // the weights (older than the prologue DMA)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          float wv[4];
+          unpack(hw[j], wv);
+#pragma unroll
+          for (int ii = 0; ii < FM; ++ii) {
+            float v[4];
+            unpack(hp[ii][j], v);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = (v[e] * hr[ii]) * wv[e];
+            hp[ii][j] = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));   // bf16(v * r * w)
+          }
+        }
+      }
+      if (hrope) {
+#pragma unroll
+        for (int i0 = 0; i0 < FM; i0 += FM / 2) {
+          load_rope(i0);
+          // all 16 loads in flight together, then one wait (without the pin hipcc sinks each load to
+          // its use and waits for it there: 16 serial L2 round trips per half)
+#pragma unroll
+          for (int ii = 0; ii < FM / 2; ++ii)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              asm volatile("" : "+v"(rc[ii][j].x), "+v"(rc[ii][j].y), "+v"(rc[ii][j].z), "+v"(rc[ii][j].w));
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int ii = 0; ii < FM / 2; ++ii)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+              float v[4];
+              unpack(hp[i0 + ii][j], v);
+              const float4 cs = rc[ii][j];
+              const float y0 = (v[0] * cs.x) - (v[1] * cs.y), y1 = (v[0] * cs.y) + (v[1] * cs.x);
+              const float y2 = (v[2] * cs.z) - (v[3] * cs.w), y3 = (v[2] * cs.w) + (v[3] * cs.z);
+              hp[i0 + ii][j] = make_uint2(pack2bf(y0, y1), pack2bf(y2, y3));
+            }
+        }
+      }
+#pragma unroll
+      for (int ii = 0; ii < FM; ++ii) {
+        const uint32_t off = (uint32_t)(((mb + ii * 16) * ldc + nb) * 2);
+#pragma unroll
+        for (int p = 0; p < FN / 2; ++p)
+          __builtin_amdgcn_raw_buffer_store_b128(swap_pair(hp[ii][2 * p], hp[ii][2 * p + 1]), crs, off + p * 64, 0, CP);
+      }
+    } else if constexpr (EK == EK_SWIGLU) {
       // gate/up column blocks interleaved by 16 (j = 2jj gate, 2jj+1 up), as gemm_epilogue; the
       // two output fragments (jj = 0, 1) form the swapped pair: 8 columns of 32 per lane
       const int nbo = n0 / 2 + wn * (TN / 2) + cpos;
@@ -1430,7 +1575,8 @@ int launch_bf16(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 
 // persistent kernel: register epilogues only, K >= 128, and 32-bit buffer offsets for C / aux
 bool ps_ok(const EchoGemmArgs* a, int ek) {
-  if (ek != EK_STORE && ek != EK_SWIGLU && ek != EK_RESID && ek != EK_BIAS) return false;
+  if (ek != EK_STORE && ek != EK_SWIGLU && ek != EK_RESID && ek != EK_BIAS && ek != EK_HEADNORM) return false;
+  if (ek == EK_HEADNORM && (a->batch != 1 || a->hn_heads <= 0)) return false;
   if (a->K < 128 || a->N % 256) return false;
   const int64_t lim = (int64_t)1 << 30;  // elements: 32-bit byte offsets (rows up to M + 255)
   if ((int64_t)(a->M + 255) * a->ldc >= lim || (int64_t)a->M * a->lda >= lim || (int64_t)a->N * a->ldw >= lim)
@@ -1446,6 +1592,7 @@ int launch_ps(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
     case EK_SWIGLU: return launch_ps_ek<EK_SWIGLU, CP>(a, ep, s);
     case EK_RESID: return launch_ps_ek<EK_RESID, CP>(a, ep, s);
     case EK_BIAS: return launch_ps_ek<EK_BIAS, CP>(a, ep, s);
+    case EK_HEADNORM: return launch_ps_ek<EK_HEADNORM, CP>(a, ep, s);
     default: return ECHO_EINVAL;
   }
 }
@@ -1528,7 +1675,10 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   // 256x256 tiles run the persistent 2-phase kernel where its register epilogue applies, else the
   // 2-phase ping-pong (all bitwise-identical results)
   if (a->tile == 0 && t == 1) t = (a->dtype == ECHO_BF16 && ps_ok(a, ek_of(a)) && !g_gemm_no_ps) ? 16 : 13;
-  if (headnorm && (a->dtype != ECHO_BF16 || t != 13 || a->N % 128)) {
+  // fused on the persistent kernel (t 16/17/18, N % 256 == 0, via ps_ok) or the 2-phase one (t 13)
+  const bool hn_fused = a->dtype == ECHO_BF16 && ((t == 13 && a->N % 128 == 0) ||
+                                                   ((t == 16 || t == 17 || t == 18) && ps_ok(a, EK_HEADNORM)));
+  if (headnorm && !hn_fused) {
     // not fused for this shape / dtype: plain store, then the standalone kernel (same results)
     EchoGemmArgs b = *a;
     b.epilogue = ECHO_EPI_STORE;

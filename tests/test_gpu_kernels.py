@@ -653,13 +653,16 @@ def test_head_norm_rope(dtype):
     assert torch.equal(x[:, 2 * H * 128:].cpu(), x0[:, 2 * H * 128:])
 
 
-@pytest.mark.parametrize("tile", [0, 13, 2])
-@pytest.mark.parametrize("M,H,pos0", [(333, 4, 5), (1280, 16, 0), (640, 16, 17)])
-def test_gemm_headnorm_fused(tile, M, H, pos0):
-    """ECHO_EPI_HEADNORM == store + echo_head_norm_rope, bitwise (fused in the 2-phase 256x256
-    epilogue for tile 13, composed inside echo_gemm otherwise)."""
+@pytest.mark.parametrize("tile", [0, 13, 16, 2])
+@pytest.mark.parametrize("M,H,pos0,rh,K", [(333, 4, 5, 2, 256), (1280, 16, 0, 8, 256), (640, 16, 17, 8, 256),
+                                          (700, 10, 0, 10, 128), (3840, 16, 3, 8, 2048)])
+def test_gemm_headnorm_fused(tile, M, H, pos0, rh, K):
+    """ECHO_EPI_HEADNORM == store + echo_head_norm_rope, bitwise: fused in the persistent kernel's
+    register epilogue (tile 16, the auto pick for 256x256 launches), in the 2-phase kernel's LDS-staged
+    epilogue (tile 13), composed inside echo_gemm otherwise. Decoder (16 heads, half RoPE) and encoder
+    (10 heads, full RoPE) layouts, partial last row tiles, position offsets."""
     from echo_tts_amd.model import rope_table_cpu
-    K, N = 256, 4 * H * 128
+    N = 4 * H * 128
     a = torch.randn(M, K, device=DEV).to(BF)
     w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
     nw = (1 + 0.1 * torch.randn(2, H, 128, device=DEV)).to(BF)
@@ -667,8 +670,8 @@ def test_gemm_headnorm_fused(tile, M, H, pos0):
     seq = 160 if M % 160 == 0 else M
     ref = ops.gemm(a, w, tile=tile)
     ops.head_norm_rope(ref, H, nw, 1e-5, nblk=2, col0=0, col_stride=H * 128, w_stride=H * 128, rope=rope,
-                       rope_heads=H // 2, seq_len=seq, pos0=pos0)
-    hn = ops.HeadNorm(nw, H, 2, 1e-5, w_stride=H * 128, rope=rope, rope_heads=H // 2, seq_len=seq, pos0=pos0)
+                       rope_heads=rh, seq_len=seq, pos0=pos0)
+    hn = ops.HeadNorm(nw, H, 2, 1e-5, w_stride=H * 128, rope=rope, rope_heads=rh, seq_len=seq, pos0=pos0)
     got = ops.gemm(a, w, tile=tile, head_norm=hn)
     assert torch.equal(got, ref)
 

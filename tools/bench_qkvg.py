@@ -1,6 +1,7 @@
 """QKVG projection of the decoder, two ways, interleaved in one process (HIP events):
-  fused  — gemm_bf16_pp2_kernel<HEADNORM>: q/k RMSNorm + half RoPE in the GEMM epilogue
-  split  — persistent store GEMM (gemm_bf16_ps_kernel<STORE>) + head_norm_rope on the q/k blocks
+  fused      — auto tile: gemm_bf16_ps_kernel<HEADNORM> (persistent, register epilogue, round 3)
+  fused_pp2  — gemm_bf16_pp2_kernel<HEADNORM>: the 2-phase kernel's LDS-staged epilogue (tile 13)
+  split      — persistent store GEMM (gemm_bf16_ps_kernel<STORE>) + head_norm_rope on the q/k blocks
 Both give bitwise-equal outputs (tests/test_gpu_kernels.py); this measures which is faster.
     python tools/bench_qkvg.py [--rounds 5]
 """
@@ -34,6 +35,9 @@ def main():
         def fused():
             ops.gemm(x, w, out=out, head_norm=hn)
 
+        def fused_pp2():
+            ops.gemm(x, w, out=out, head_norm=hn, tile=13)
+
         def split():
             ops.gemm(x, w, out=out)
             ops.head_norm_rope(out, H, qk, 1e-5, nblk=2, col0=0, col_stride=D, w_stride=H * 128, rope=rope,
@@ -49,7 +53,10 @@ def main():
         a = out.clone()
         split()
         same = bool(torch.equal(a, out))
-        arms = (("fused", fused), ("split", split), ("store_ps", store_ps), ("store_pp2", store_pp2))
+        fused_pp2()
+        same = same and bool(torch.equal(a, out))
+        arms = (("fused", fused), ("fused_pp2", fused_pp2), ("split", split), ("store_ps", store_ps),
+                ("store_pp2", store_pp2))
         times = {k: [] for k, _ in arms}
         for _ in range(args.rounds):
             for name, fn in arms:
