@@ -700,6 +700,211 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
   }
 }
 
+// ----------------------------------------------------------------------------- asm-owned pipeline
+// attn_pl_kernel: attn_bf16_kernel<0, 4, 2>'s math in the same order (bitwise-equal output), with the
+// tile loop software-pipelined by hand (cdna_hip_programming.md T15) over registers the compiler does
+// not own: amdgpu_num_vgpr(96) caps hipcc at v0..v95 and the tile bodies (attn_pl.inc, generated by
+// tools/gen_attn_pl.py) keep O, two score buffers and the K / V^T fragment rings in v96..v255. Per tile t:
+//   X(t): softmax of tile t (fma, exp2, row sum, bf16 pack of P in place)  ||  QK of tile t+1 (16 MFMA)
+//   Y(t): PV of tile t (16 MFMA)  ||  prefix mask (partial tiles) + row max of tile t+1
+// then the deferred-max decision for t+1 (rare O rescale), the wave's DMA wait and ONE barrier.
+// hipcc's own allocation of the production kernel copies O (32 v_mov_b64) and the scores (32 v_mov_b32)
+// across the rescale / mask branch joins on every tile; here no loop state crosses a compiler join.
+// K and V have separate 2-slot rings ([K0 | K1 | V0 | V1], 16 KB each): K(t+2) and V(t+1) are issued
+// at the top of iteration t into the slots that K(t) and V(t-1) left (read before the previous
+// barrier) and waited for at its end. Non-causal segments only (decoder attention); the host routes
+// causal launches (speaker / latent encoders) to attn_bf16_kernel.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+#include "attn_pl.inc"
+
+// ABL (timing ablations, variants 12-16; results wrong): 1 no loop DMA, 2 no X body, 4 no Y body,
+// 8 no end-of-tile wait + barrier, 16 no tile loop
+template <int ABL>
+__global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_num_vgpr(96)))
+    attn_pl_kernel(EchoAttnArgs a_arg) {
+  constexpr int NW = 4, QB = 128, DPT = 4, KTT = KT;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[4 * KT * 128];  // K slot 0, 1 | V slot 0, 1
+
+  using KArgs = const __attribute__((address_space(4))) EchoAttnArgs;
+  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  (void)a_arg;
+  const int nqb = (a.n_q + QB - 1) / QB;
+  const int L = remap_xcd(blockIdx.x, gridDim.x);
+  const int qb = L % nqb;
+  const int Lr = L / nqb;  // rows fastest (see attn_bf16_kernel)
+  const int row = Lr % a.rows;
+  const int head = Lr / a.rows;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h2 = lane >> 5, ql = lane & 31;
+  const int q0 = qb * QB;
+  const int qc = min(q0 + w * 32 + ql, a.n_q - 1);
+
+  const bf16_t* qp = (const bf16_t*)a.q + ECHO_QROW(a, row) * a.q_ld_batch + (int64_t)qc * a.q_ld_tok + head * 128;
+  bf16x8 qf[8];
+#pragma unroll
+  for (int ds = 0; ds < 8; ++ds) qf[ds] = *(const bf16x8*)(qp + 16 * ds + 8 * h2);
+#pragma unroll
+  for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));  // one wait for Q, before any DMA
+
+  ECHO_SEG_TABLE()
+  ECHO_CURSOR_ADVANCE()
+  Cursor kc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // K DMA (two tiles ahead of PV)
+  Cursor vc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // V DMA (one tile ahead)
+  Cursor mc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // the tile whose scores are masked / maxed
+
+  const int dr = lane >> 4, dp = lane & 15;
+  auto dma_part = [&](Cursor& c, int part, int slot) __attribute__((always_inline)) {
+    advance(c);
+    const int last = c.kend - 1 - c.t0;
+    const bf16_t* base = (part ? c.vb : c.kb) + (int64_t)c.t0 * c.ld;
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int r = (i * NW + w) * 4 + dr;
+      const uint32_t voff = (uint32_t)(min(r, last) * c.ld + ((dp ^ swz(r)) * 8)) * 2u;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          lds_addr_of(lds + (part * 2 + slot) * KT * 128 + ((i * NW + w) * 4) * 128));
+      glds16s(base, voff, dst);
+    }
+  };
+
+  // per-lane LDS byte addresses of the fragment reads (slot / sub-tile offsets are immediates):
+  // K row kk*32 + ql, chunk (2 ds + h2) ^ swz; V^T rows r0 = 4 h2 + q4 (+ 8) of chunk 4 dt + ...
+  const uint32_t lbase = lds_addr_of(lds);
+  uint32_t ka[8], va[8];
+#pragma unroll
+  for (int ds = 0; ds < 8; ++ds) ka[ds] = lbase + (uint32_t)(ql * 128 + (((2 * ds + h2) ^ swz(ql)) * 8)) * 2u;
+  {
+    const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+    const int r0 = 4 * h2 + q4, r1 = r0 + 8;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int ch = 4 * dt + 2 * (g & 1) + (p4 >> 1);
+      va[2 * dt] = lbase + 2u * KT * 128 * 2 + (uint32_t)(r0 * 128 + ((ch ^ swz(r0)) * 8) + (p4 & 1) * 4) * 2u;
+      va[2 * dt + 1] = lbase + 2u * KT * 128 * 2 + (uint32_t)(r1 * 128 + ((ch ^ swz(r1)) * 8) + (p4 & 1) * 4) * 2u;
+    }
+  }
+
+  float m_run = -INFINITY, l_run = 0.f;
+  const float sl2 = a.scale * 1.4426950408889634f;
+  const int hb = 4 * h2;
+  // prefix mask of the next tile (cursor mc advanced to it) if it is partial
+  auto mask_tile = [&](auto par) __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value;
+    advance(mc);
+    const int lim = mc.kend - mc.t0;
+    if (lim < KTT) {
+      if constexpr (P == 0) pl_mask_0(lim, hb); else pl_mask_1(lim, hb);
+    }
+  };
+  // the deferred running-max decision of attn_bf16_kernel for a tile with lane max mx
+  auto decide = [&](float mx) __attribute__((always_inline)) {
+    mx = halves_max(mx);
+    if (__any(m_run == -INFINITY || (mx - m_run) * sl2 > 8.0f)) {
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha =
+          __builtin_amdgcn_exp2f(__builtin_fmaf(m_run, sl2, m_new == -INFINITY ? 0.f : -m_new * sl2));
+      l_run *= alpha;
+      pl_rescale(alpha);
+      m_run = m_new;
+    }
+  };
+
+  pl_zero_o();
+  // prologue: K(0), V(0), K(1); scores, mask and max of tile 0
+  if (ntiles > 0) { dma_part(kc, 0, 0); dma_part(vc, 1, 0); }
+  if (ntiles > 1) dma_part(kc, 0, 1);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  if (ntiles > 0) {
+    pl_qk_0(qf, ka);
+    mask_tile(std::integral_constant<int, 0>{});
+    float mx, ma;
+    pl_max_0(mx, ma);
+    decide(mx);
+  }
+  asm volatile("s_barrier" ::: "memory");  // every wave's K(0) reads are done: slot 0 takes K(2)
+
+  auto iter = [&](int t, auto par) __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value;
+    if (t + 2 < ntiles && !(ABL & 1)) dma_part(kc, 0, P);      // K(t+2) -> K slot t & 1 (K(t) was read in X(t-1))
+    if (t + 1 < ntiles && !(ABL & 1)) dma_part(vc, 1, 1 - P);  // V(t+1) -> V slot (t+1) & 1 (V(t-1) was read in Y(t-1))
+    const float msc = m_run == -INFINITY ? 0.f : -m_run * sl2;
+    float ps;
+    if (t + 1 < ntiles) {
+      ps = 0.f;
+      if constexpr (!(ABL & 2)) { if constexpr (P == 0) pl_x_0(qf, ka, sl2, msc, ps); else pl_x_1(qf, ka, sl2, msc, ps); }
+      l_run += ps;
+      mask_tile(std::integral_constant<int, 1 - P>{});
+      float mx = 0.f, ma;
+      if constexpr (!(ABL & 4)) { if constexpr (P == 0) pl_y_0(va, mx, ma); else pl_y_1(va, mx, ma); }
+      decide(mx);
+    } else {
+      if constexpr (P == 0) pl_xl_0(sl2, msc, ps); else pl_xl_1(sl2, msc, ps);
+      l_run += ps;
+      if constexpr (P == 0) pl_yl_0(va); else pl_yl_1(va);
+    }
+    if constexpr (!(ABL & 8)) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  if (ABL & 16) ntiles = 0;
+  for (int t = 0; t < ntiles; t += 2) {
+    iter(t, std::integral_constant<int, 0>{});
+    if (t + 1 >= ntiles) break;
+    iter(t + 1, std::integral_constant<int, 1>{});
+  }
+
+  // ---- epilogue (attn_bf16_kernel's row layout): normalise, round, transpose through LDS, gate, store
+  const float lt = halves_sum(l_run);
+  const float inv = 1.0f / lt;
+  const int nv = a.n_q - (q0 + w * 32);  // wave-uniform
+  if (nv > 0) {
+    uint4 v4[8];
+    auto pack_dt = [&](const float (&od)[16], int dt) __attribute__((always_inline)) {
+      uint32_t wd[4][2];
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        wd[rg][0] = pack2bf(rbf(od[4 * rg + 0] * inv), rbf(od[4 * rg + 1] * inv));
+        wd[rg][1] = pack2bf(rbf(od[4 * rg + 2] * inv), rbf(od[4 * rg + 3] * inv));
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const auto x = __builtin_amdgcn_permlane32_swap(wd[2 * k][0], wd[2 * k + 1][0], false, false);
+        const auto y = __builtin_amdgcn_permlane32_swap(wd[2 * k][1], wd[2 * k + 1][1], false, false);
+        v4[2 * dt + k] = make_uint4(x[0], y[0], x[1], y[1]);
+      }
+    };
+    {
+      float od[16];
+      pl_get_o_0(od); pack_dt(od, 0);
+      pl_get_o_1(od); pack_dt(od, 1);
+      pl_get_o_2(od); pack_dt(od, 2);
+      pl_get_o_3(od); pack_dt(od, 3);
+    }
+    const int rl = lane >> 4, cc = lane & 15;
+    const int64_t qw = q0 + w * 32;
+    uint4 g4[8];
+    if (a.gate) {
+      const __amdgpu_buffer_rsrc_t gr =
+          attn_rsrc((const bf16_t*)a.gate + ECHO_QROW(a, row) * a.g_ld_batch + qw * a.g_ld_tok + head * 128,
+                    (uint32_t)(((int64_t)(min(nv, 32) - 1) * a.g_ld_tok + 128) * 2));
+      const uint32_t glo = (uint32_t)((rl * a.g_ld_tok + cc * 8) * 2), gst = (uint32_t)(a.g_ld_tok * 8);
+#pragma unroll
+      for (int pk = 0; pk < 8; ++pk) g4[pk] = attn_bload(gr, glo + pk * gst);
+    }
+    bf16_t* sw = lds + w * 32 * 128;  // free: no DMA in flight, every wave passed the last barrier
+#pragma unroll
+    for (int pk = 0; pk < 8; ++pk) *(uint4*)(sw + ql * 128 + (((2 * pk + h2) ^ (ql & 15)) * 8)) = v4[pk];
+#pragma unroll
+    for (int pk = 0; pk < 8; ++pk) {
+      const int r = pk * 4 + rl;
+      v4[pk] = *(const uint4*)(sw + r * 128 + ((cc ^ (r & 15)) * 8));
+    }
+    if (a.gate) attn_gate(v4, g4);
+    attn_store_rows(v4, (bf16_t*)a.out + row * a.o_ld_batch + qw * a.o_ld_tok + head * 128, nv, a.o_ld_tok, lane);
+  }
+}
+#pragma clang diagnostic pop
+
 // ----------------------------------------------------------------------------- software-pipelined
 // Same tile math, LDS image and numerics as attn_bf16_kernel<0,4,2>, scheduled so that every wave
 // overlaps its own MFMA and VALU work (cdna_hip_programming.md T15), two workgroups per CU:
@@ -1082,6 +1287,14 @@ int check_attn_args(const EchoAttnArgs* a) {
 
 int attn_grid(const EchoAttnArgs* a, int qb) { return ((a->n_q + qb - 1) / qb) * a->heads * a->rows; }
 
+bool any_causal(const EchoAttnArgs* a) {
+  for (int s = 0; s < a->nseg; ++s)
+    if (a->seg[s].k && a->seg[s].causal) return true;
+  return false;
+}
+
+int g_attn_pl = 1;  // echo_attention_set_pipeline: 0 = attn_bf16_kernel for every launch (A/B)
+
 // persistent grid: two workgroups per CU (a multiple of 8, so an item's XCD is its block's XCD)
 int attn_ps_grid(int nitems) {
   static int cus = 0;
@@ -1151,6 +1364,16 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       break;
     case 7: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 3, 32); break;
     case 10: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(2048, 4, 2); break;  // per-lane epilogue
+    case 11:  // asm-owned software pipeline (production for non-causal launches)
+      if (abl || any_causal(a)) return ECHO_EINVAL;
+      hipLaunchKernelGGL(attn_pl_kernel<0>, grid, dim3(256), 0, s, *a);
+      break;
+    case 12: hipLaunchKernelGGL(attn_pl_kernel<1>, grid, dim3(256), 0, s, *a); break;
+    case 13: hipLaunchKernelGGL(attn_pl_kernel<2>, grid, dim3(256), 0, s, *a); break;
+    case 14: hipLaunchKernelGGL(attn_pl_kernel<4>, grid, dim3(256), 0, s, *a); break;
+    case 15: hipLaunchKernelGGL(attn_pl_kernel<8>, grid, dim3(256), 0, s, *a); break;
+    case 16: hipLaunchKernelGGL(attn_pl_kernel<16>, grid, dim3(256), 0, s, *a); break;
+    case 17: hipLaunchKernelGGL(attn_pl_kernel<6>, grid, dim3(256), 0, s, *a); break;
     default: return ECHO_EINVAL;
   }
 #undef ECHO_ATTN_ABLS
@@ -1173,7 +1396,12 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
     // (fewer items than CUs, B = 1: 64-query workgroups — variant 9, bitwise equal — are slower,
     // R = 3: 43.2 -> 54.1 us, R = 1: 38.7 -> 47.1 us: the per-workgroup tile chain stays as long and
     // each wave issues twice the DMA; that case takes split-KV chains, echo_attention_split)
-    hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1);
+    // non-causal launches (every decoder attention) run the asm-owned pipeline (attn_pl_kernel, bitwise
+    // equal to attn_bf16_kernel<0, 4, 2>); causal ones (speaker / latent encoders) the compiler-scheduled kernel
+    if (g_attn_pl && !any_causal(a))
+      hipLaunchKernelGGL(attn_pl_kernel<0>, dim3(attn_grid(a, 128)), dim3(256), 0, s, *a);
+    else
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1);
   } else {
     hipLaunchKernelGGL(attn_f32_kernel, dim3(attn_grid(a, FQ)), dim3(64), 0, s, *a);
   }
@@ -1222,6 +1450,12 @@ extern "C" int32_t echo_attention_pick_split(const EchoAttnArgs* a) {
     nsp = min(nsp, tiles / 3);
   }
   return max(1, min(nsp, min(tiles, 16)));
+}
+
+extern "C" int echo_attention_set_pipeline(int32_t on) {
+  if (on < 0 || on > 1) return ECHO_EINVAL;
+  g_attn_pl = on;
+  return 0;
 }
 
 extern "C" int echo_attention_set_split(int32_t nsplit) {

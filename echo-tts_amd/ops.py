@@ -147,6 +147,19 @@ def attention_split(nsplit: int):
         lib().echo_attention_set_split(-1)
 
 
+@contextlib.contextmanager
+def attention_pipeline(on: bool):
+    """Route non-causal bf16 attention launches to the asm-owned pipelined kernel (True, the default)
+    or to the compiler-scheduled kernel (False) inside the block (A/B tests and measurements)."""
+    rc = lib().echo_attention_set_pipeline(int(bool(on)))
+    if rc:
+        raise RuntimeError(f"echo_attention_set_pipeline({on}) failed: {rc}")
+    try:
+        yield
+    finally:
+        lib().echo_attention_set_pipeline(1)
+
+
 def attention_variant(q: Tensor, segments: Sequence[Segment], out: Tensor, gate: Optional[Tensor] = None,
                       scale: float = 128 ** -0.5, *, variant: int = 0, ablation: int = 0,
                       stamps: Optional[Tensor] = None) -> Tensor:

@@ -137,6 +137,10 @@ int64_t echo_attention_split_ws_bytes(const EchoAttnArgs* args, int32_t nsplit);
 int32_t echo_attention_pick_split(const EchoAttnArgs* args);
 /* Diagnostics: force the policy's answer (0/1 = never split, 2..16), -1 = back to the policy. */
 int echo_attention_set_split(int32_t nsplit);
+/* Diagnostics: 1 (default) = non-causal bf16 launches run the asm-owned software-pipelined kernel
+ * (attn_pl_kernel, bitwise equal to the compiler-scheduled one), 0 = the compiler-scheduled kernel for
+ * every launch (A/B measurements). */
+int echo_attention_set_pipeline(int32_t on);
 
 /* Diagnostics only (tools/bench_attn.py, tools/attn_timeline.py; never on the sampling path):
  * measurement variants of the bf16 attention kernel. variant 0 = the production kernel;

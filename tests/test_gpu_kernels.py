@@ -443,6 +443,62 @@ def test_attention_persistent_multi_item(n_q, cfg):
     assert torch.equal(got, ref)
 
 
+def _pipeline_case(case):
+    """Segment sets for the asm-owned pipeline test: the sampler's CFG / plain launches, ragged and
+    empty text rows, a 1-tile item, a 1-query launch, segments shorter than a tile, spiky scores."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    rn = lambda *s: torch.randn(*s, device=DEV, generator=g)
+    if case in ("cfg640", "plain600"):
+        B, H, T, P = 4, 16, 448, 160
+        n_q, R = (640, 3 * B) if case == "cfg640" else (600, B)
+        qkvg, kt, ks = rn(R, n_q, 4, H, 128).to(BF), rn(B, T, 2, H, 128).to(BF), rn(B, P, 2, H, 128).to(BF)
+        tl = torch.tensor(([388, 0, 201, 448] + [0] * B + [388, 0, 201, 448])[:R], dtype=torch.int32, device=DEV)
+        sl = torch.tensor(([P] * 2 * B + [0] * B)[:R], dtype=torch.int32, device=DEV)
+        segs = [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2]),
+                ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=tl, batch_mod=B),
+                ops.Segment(ks[:, :, 0], ks[:, :, 1], lens=sl, batch_mod=B)]
+        return qkvg, segs, qkvg[:, :, 3]
+    if case == "one_tile":      # every item has exactly one (partial) tile
+        qkvg = rn(2, 50, 4, 3, 128).to(BF)
+        return qkvg, [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2])], qkvg[:, :, 3]
+    if case == "one_query":     # n_q = 1, three short segments (1, 63, 65 keys)
+        qkvg, a, b = rn(1, 1, 4, 2, 128).to(BF), rn(1, 63, 2, 2, 128).to(BF), rn(1, 65, 2, 2, 128).to(BF)
+        return qkvg, [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2]), ops.Segment(a[:, :, 0], a[:, :, 1]),
+                      ops.Segment(b[:, :, 0], b[:, :, 1])], None
+    if case == "spikes":        # scores jumping by up to ~60 exp2 units: the O rescale at many tiles
+        qkvg = rn(3, 300, 4, 5, 128)
+        qkvg[:, ::37, 1] *= 12.0
+        qkvg = qkvg.to(BF)
+        lens = torch.tensor([300, 257, 64], dtype=torch.int32, device=DEV)
+        return qkvg, [ops.Segment(qkvg[:, :, 1], qkvg[:, :, 2], lens=lens)], qkvg[:, :, 3]
+    raise ValueError(case)
+
+
+@pytest.mark.parametrize("case", ["cfg640", "plain600", "one_tile", "one_query", "spikes"])
+def test_attention_pipeline_bitwise(case):
+    """The asm-owned software-pipelined kernel (attn_pl_kernel: production for non-causal launches,
+    variant 11) computes attn_bf16_kernel<0, 4, 2>'s math in the same order: bitwise equal to variant 0,
+    through ops.attention and the variant entry, with and without a gate; close to fp64."""
+    q, segs, gate = _pipeline_case(case)
+    R, n_q, H = q.shape[0], q.shape[1], q.shape[3]
+    ref = torch.full((R, n_q, H, 128), float("nan"), device=DEV, dtype=BF)
+    ops.attention_variant(q[:, :, 0], segs, out=ref, gate=gate, variant=0)
+    got = torch.full_like(ref, float("nan"))
+    ops.attention_variant(q[:, :, 0], segs, out=got, gate=gate, variant=11)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), float((got != ref).double().mean())
+    got.fill_(float("nan"))
+    with ops.attention_split(1):
+        ops.attention(q[:, :, 0], segs, out=got, gate=gate)
+    assert torch.equal(got, ref)
+    with ops.attention_pipeline(False), ops.attention_split(1):
+        got.fill_(float("nan"))
+        ops.attention(q[:, :, 0], segs, out=got, gate=gate)
+    assert torch.equal(got, ref)
+    if case in ("one_tile", "one_query", "spikes"):
+        close_bf16(ref, ref_attention(q[:, :, 0], segs, gate, 128 ** -0.5, BF))
+
+
 def test_attention_engine_kv_layout():
     """The engine's KV layout: one [B, T, 24, 2, H, 128] buffer per stream, layer = strided view
     (1.4 GB for B=16, T=448): tile base addresses span > 2^31 bytes, so any 32-bit address word
