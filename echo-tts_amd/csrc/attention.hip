@@ -718,8 +718,9 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
 #pragma clang diagnostic ignored "-Winline-asm"
 #include "attn_pl.inc"
 
-// ABL (timing ablations, variants 12-16; results wrong): 1 no loop DMA, 2 no X body, 4 no Y body,
-// 8 no end-of-tile wait + barrier, 16 no tile loop
+// ABL (timing ablations, variants 12-19; results wrong except 32): 1 no loop DMA, 2 no X body, 4 no Y body,
+// 8 no end-of-tile wait + barrier, 16 no tile loop; 32 (diagnostic, results right): CFG rows of one prompt
+// (r, r + B, r + 2B; B = segment 1's batch_mod) adjacent in the block order
 template <int ABL>
 __global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_num_vgpr(96)))
     attn_pl_kernel(EchoAttnArgs a_arg) {
@@ -733,7 +734,11 @@ __global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_num_vgpr(96)))
   const int L = remap_xcd(blockIdx.x, gridDim.x);
   const int qb = L % nqb;
   const int Lr = L / nqb;  // rows fastest (see attn_bf16_kernel)
-  const int row = Lr % a.rows;
+  int row = Lr % a.rows;
+  if constexpr ((ABL & 32) != 0) {
+    const int B = a.nseg > 1 ? a.seg[1].batch_mod : a.rows;
+    if (a.rows == 3 * B) row = (row % 3) * B + row / 3;
+  }
   const int head = Lr / a.rows;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -745,8 +750,6 @@ __global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_num_vgpr(96)))
   bf16x8 qf[8];
 #pragma unroll
   for (int ds = 0; ds < 8; ++ds) qf[ds] = *(const bf16x8*)(qp + 16 * ds + 8 * h2);
-#pragma unroll
-  for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));  // one wait for Q, before any DMA
 
   ECHO_SEG_TABLE()
   ECHO_CURSOR_ADVANCE()
@@ -815,6 +818,9 @@ __global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_num_vgpr(96)))
   // prologue: K(0), V(0), K(1); scores, mask and max of tile 0
   if (ntiles > 0) { dma_part(kc, 0, 0); dma_part(vc, 1, 0); }
   if (ntiles > 1) dma_part(kc, 0, 1);
+  // Q and the prologue DMA in flight together: one wait (hipcc's vmcnt(0) for Q covers the DMA issued after it)
+#pragma unroll
+  for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   if (ntiles > 0) {
     pl_qk_0(qf, ka);
@@ -873,23 +879,23 @@ __global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_num_vgpr(96)))
         v4[2 * dt + k] = make_uint4(x[0], y[0], x[1], y[1]);
       }
     };
-    {
-      float od[16];
-      pl_get_o_0(od); pack_dt(od, 0);
-      pl_get_o_1(od); pack_dt(od, 1);
-      pl_get_o_2(od); pack_dt(od, 2);
-      pl_get_o_3(od); pack_dt(od, 3);
-    }
     const int rl = lane >> 4, cc = lane & 15;
     const int64_t qw = q0 + w * 32;
     uint4 g4[8];
-    if (a.gate) {
+    if (a.gate) {  // in flight during the pack and the transposition
       const __amdgpu_buffer_rsrc_t gr =
           attn_rsrc((const bf16_t*)a.gate + ECHO_QROW(a, row) * a.g_ld_batch + qw * a.g_ld_tok + head * 128,
                     (uint32_t)(((int64_t)(min(nv, 32) - 1) * a.g_ld_tok + 128) * 2));
       const uint32_t glo = (uint32_t)((rl * a.g_ld_tok + cc * 8) * 2), gst = (uint32_t)(a.g_ld_tok * 8);
 #pragma unroll
       for (int pk = 0; pk < 8; ++pk) g4[pk] = attn_bload(gr, glo + pk * gst);
+    }
+    {
+      float od[16];
+      pl_get_o_0(od); pack_dt(od, 0);
+      pl_get_o_1(od); pack_dt(od, 1);
+      pl_get_o_2(od); pack_dt(od, 2);
+      pl_get_o_3(od); pack_dt(od, 3);
     }
     bf16_t* sw = lds + w * 32 * 128;  // free: no DMA in flight, every wave passed the last barrier
 #pragma unroll
@@ -1374,6 +1380,8 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 15: hipLaunchKernelGGL(attn_pl_kernel<8>, grid, dim3(256), 0, s, *a); break;
     case 16: hipLaunchKernelGGL(attn_pl_kernel<16>, grid, dim3(256), 0, s, *a); break;
     case 17: hipLaunchKernelGGL(attn_pl_kernel<6>, grid, dim3(256), 0, s, *a); break;
+    case 18: hipLaunchKernelGGL(attn_pl_kernel<7>, grid, dim3(256), 0, s, *a); break;
+    case 19: hipLaunchKernelGGL(attn_pl_kernel<32>, grid, dim3(256), 0, s, *a); break;
     default: return ECHO_EINVAL;
   }
 #undef ECHO_ATTN_ABLS
