@@ -117,6 +117,11 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         fn = getattr(lib, name)  # AttributeError if a declared symbol is missing
         fn.restype, fn.argtypes = res, args
     _lib = lib
+    # A/B measurements only: ECHO_GEMM_DIAG="key=value,..." -> echo_gemm_set_diag (keys: echo_hip.h)
+    for kv in filter(None, os.environ.get("ECHO_GEMM_DIAG", "").split(",")):
+        k, v = (int(x) for x in kv.split("="))
+        if lib.echo_gemm_set_diag(k, v) != 0:
+            raise RuntimeError(f"ECHO_GEMM_DIAG: echo_gemm_set_diag({k}, {v}) failed")
     return lib
 
 

@@ -1221,6 +1221,196 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   }
 }
 
+// ----------------------------------------------------------------------------- 320 x 256 tile
+// gemm_bf16_t320_kernel<EK_RESID>: 320x256x64 tiles for the N = 2048 gated-residual GEMMs (Wo, W2), whose
+// 256x256 tile count leaves a partial last round at the decoder's M (M = 30720: 960 tiles = 3.75 rounds of
+// 256 CUs, M = 10240: 1.25 rounds) while 320-row tiles divide it exactly (768 / 256 tiles = 3 / 1 rounds).
+// Same fragments, MFMA and per-element K order as the 256x256 kernels: bitwise-equal results, so the
+// B = 16 rows still equal B = 1 runs. 8 waves as 4 (M) x 2 (N), 80 x 128 outputs per wave:
+//   phase 0: the wave's 5 x 2 A fragments (held for the K-tile) x its W columns 0-63   (40 MFMA)
+//   phase 1: the same A fragments x its W columns 64-127                                (40 MFMA)
+// LDS stage = A 320 x 64 | W 256 x 64 (72 KB), 2 stages. DMA chunks (1 KiB wave-instructions, the
+// source-side swizzle of the other kernels): cA = all A rows (5 per wave), cW0 = the W rows phase 0 reads
+// (2 per wave), cW1 = phase 1's (2 per wave). cA + cW0 of K-tile k+2 are issued in phase 1 of tile k,
+// cW1 of tile k+1 in phase 0 of tile k: gemm_bf16_pp2_kernel's schedule and barrier argument with
+// c0-c2 -> cA + cW0 and c3 -> cW1, so the steady-state waits are vmcnt(9) (2 + 7 younger pieces).
+// Epilogue from registers, row fragment by row fragment (the residual rows of the next one in flight).
+template <int EK>
+__global__ void __launch_bounds__(512)
+gemm_bf16_t320_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw,
+                      void* __restrict__ Cv, int64_t ldc, int M, int N, int K, int tiles_m, int tiles_n, Epi ep) {
+  static_assert(EK == EK_RESID, "320-row tiles: gated residual epilogue");
+  constexpr int BM = 320, BN = 256, TM = 80, TN = 128, FM = 5, FN = 8;
+  constexpr int STAGE = (BM + BN) * BK;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int grp = wid >> 2;  // ping-pong group: waves 4-7 run one barrier behind
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  constexpr int GM = 8;
+  const int gq = wg / (GM * tiles_n);
+  const int fm = gq * GM;
+  const int gm = min(tiles_m - fm, GM);
+  const int rem = wg - gq * GM * tiles_n;
+  const int m0 = (fm + rem % gm) * BM, n0 = (rem / gm) * BN;
+
+  // per-lane source offsets of an 8-row group (row rb + lane/8, chunk (lane&7) ^ ((row>>1)&7)); the
+  // swizzle term depends only on the group's parity (rb/8 odd adds 4)
+  const int l8 = lane >> 3;
+  uint32_t vA[2], vW[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int gc = (lane & 7) ^ ((4 * par + (l8 >> 1)) & 7);
+    vA[par] = (uint32_t)((l8 * lda + gc * 8) * 2);
+    vW[par] = (uint32_t)((l8 * ldw + gc * 8) * 2);
+  }
+  const uint32_t lds0 = lds_addr_of(lds);
+  const bf16_t* Ab = A + (int64_t)m0 * lda;
+  const bf16_t* Wb = W + (int64_t)n0 * ldw;
+  // chunk c (0 = cA, 1 = cW0, 2 = cW1) of K-tile kt into stage kt & 1
+  auto dma = [&](int c, int kt) __attribute__((always_inline)) {
+    const uint32_t st = lds0 + (uint32_t)((kt & 1) * STAGE * 2);
+    if (c == 0) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const int rb = (q * 8 + wid) * 8;
+        glds16s(Ab + (int64_t)rb * lda + kt * BK, vA[(rb >> 3) & 1], __builtin_amdgcn_readfirstlane(st + rb * BK * 2));
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int g = h * 8 + wid;
+        const int rb = (g < 8 ? g * 8 : 128 + (g - 8) * 8) + (c == 2 ? 64 : 0);
+        glds16s(Wb + (int64_t)rb * ldw + kt * BK, vW[(rb >> 3) & 1],
+                __builtin_amdgcn_readfirstlane(st + (BM + rb) * BK * 2));
+      }
+    }
+  };
+
+  const int nk = K / BK;
+  // prologue: tile 0 (cA, cW0, then cW1) and cA + cW0 of tile 1; wait for tile 0's cA + cW0
+  dma(0, 0); dma(1, 0); dma(2, 0);
+  if (nk > 1) {
+    dma(0, 1); dma(1, 1);
+    vm_wait_n<9>();
+  } else {
+    vm_wait_n<2>();
+  }
+  pp_barrier();
+  if (grp == 1) pp_barrier();
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int frow = lane & 15;
+  const int fsw = frow >> 1;
+  bf16x8 af[FM][2], bfr[4][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const bf16_t* As = lds + (kt & 1) * STAGE;
+    const bf16_t* Bs = As + BM * BK;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      // ---- L segment
+      if (ph == 0) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            af[i][s] = *(const bf16x8*)(As + (wm * TM + i * 16 + frow) * BK + (((4 * s + (lane >> 4)) ^ fsw) * 8));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          bfr[j][s] = *(const bf16x8*)(Bs + (wn * TN + ph * 64 + j * 16 + frow) * BK +
+                                       (((4 * s + (lane >> 4)) ^ fsw) * 8));
+      if (ph == 0) {
+        if (n1) dma(2, kt + 1);
+        // retire cW1 of tile kt (issued in phase 0 of tile kt-1 / the prologue)
+        if (n1) vm_wait_n<9>(); else vm_wait_n<0>();
+      } else {
+        if (n2) { dma(0, kt + 2); dma(1, kt + 2); }
+        // retire cA + cW0 of tile kt+1
+        if (n2) vm_wait_n<9>(); else if (n1) vm_wait_n<2>(); else vm_wait_n<0>();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      pp_barrier();
+      // ---- C segment
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            acc[i][ph * 4 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][s], af[i][s], acc[i][ph * 4 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+    }
+  }
+  if (grp == 0) pp_barrier();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- epilogue: out = bf16(x + bf16(g * bf16(acc))) (the persistent kernel's RESID kind). A lane holds
+  // rows mb + 16 ii, columns 16 j + 4 (lane >> 4) .. + 3 of the wave's 128; one v_permlane16_swap per
+  // packed word of a fragment pair (2p, 2p+1) gives it 8 consecutive columns (16-B accesses).
+  const int g4 = lane >> 4;
+  const int cpos = (g4 & 1) * 16 + (g4 >> 1) * 8;
+  const int mb = m0 + wm * TM + (lane & 15);
+  const int nb = n0 + wn * TN + cpos;
+  const __amdgpu_buffer_rsrc_t crs = brsrc(Cv, (uint32_t)(((int64_t)(M - 1) * ldc + N) * 2));
+  const __amdgpu_buffer_rsrc_t ars = brsrc(ep.aux, (uint32_t)(((int64_t)(M - 1) * ep.ld_aux + N) * 2));
+  auto swap_pair = [&](uint2 lo, uint2 hi) __attribute__((always_inline)) -> u32x4 {
+    const auto s0 = __builtin_amdgcn_permlane16_swap(lo.x, hi.x, false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(lo.y, hi.y, false, false);
+    return u32x4{s0[0], s1[0], s0[1], s1[1]};
+  };
+  u32x4 gv[FN / 2];
+  if (ep.gate) {
+#pragma unroll
+    for (int p = 0; p < FN / 2; ++p) gv[p] = *(const u32x4*)((const bf16_t*)ep.gate + nb + p * 32);
+  }
+  u32x4 xr[2][FN / 2];
+  auto load_x = [&](int ii, u32x4 (&d)[FN / 2]) __attribute__((always_inline)) {
+    const uint32_t off = (uint32_t)(((mb + ii * 16) * ep.ld_aux + nb) * 2);
+#pragma unroll
+    for (int p = 0; p < FN / 2; ++p)
+      d[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ars, off + p * 64, 0, 0));
+  };
+  load_x(0, xr[0]);
+#pragma unroll
+  for (int ii = 0; ii < FM; ++ii) {
+    if (ii + 1 < FM) load_x(ii + 1, xr[(ii + 1) & 1]);
+    const uint32_t off = (uint32_t)(((mb + ii * 16) * ldc + nb) * 2);
+#pragma unroll
+    for (int p = 0; p < FN / 2; ++p) {
+      const f32x4 c0 = acc[ii][2 * p], c1 = acc[ii][2 * p + 1];
+      u32x4 o = swap_pair(make_uint2(pack2bf(c0[0], c0[1]), pack2bf(c0[2], c0[3])),
+                          make_uint2(pack2bf(c1[0], c1[1]), pack2bf(c1[2], c1[3])));
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        float v0 = bf2f(o[w] & 0xffffu), v1 = bf2f(o[w] >> 16);
+        if (ep.gate) {
+          v0 = rbf(bf2f(gv[p][w] & 0xffffu) * v0);
+          v1 = rbf(bf2f(gv[p][w] >> 16) * v1);
+        }
+        v0 = bf2f(xr[ii & 1][p][w] & 0xffffu) + v0;
+        v1 = bf2f(xr[ii & 1][p][w] >> 16) + v1;
+        o[w] = pack2bf(v0, v1);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(o, crs, off + p * 64, 0, 0);
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------- fp32 (parity mode)
 constexpr int FT = 64, FK = 16;
 
@@ -1618,6 +1808,39 @@ int launch_pp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   }
 }
 
+int cu_count_cached() {
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      return 256;
+    g_num_cus = n;
+  }
+  return g_num_cus;
+}
+
+// 320x256 tiles (gemm_bf16_t320_kernel): gated residual, M % 320 == 0, 32-bit buffer offsets, 16-B aligned
+bool t320_ok(const EchoGemmArgs* a) {
+  if (a->dtype != ECHO_BF16 || ek_of(a) != EK_RESID || a->batch != 1 || a->conv_taps > 0) return false;
+  if (a->M % 320 || a->N % 256 || a->K % 64 || a->K < 128) return false;
+  const int64_t lim = (int64_t)1 << 30;
+  if ((int64_t)a->M * a->ldc >= lim || (int64_t)a->M * a->ld_aux >= lim || (int64_t)a->M * a->lda >= lim ||
+      (int64_t)a->N * a->ldw >= lim)
+    return false;
+  if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C | (uintptr_t)a->aux | (uintptr_t)a->gate) & 15) return false;
+  return a->lda % 8 == 0 && a->ldw % 8 == 0 && a->ldc % 8 == 0 && a->ld_aux % 8 == 0;
+}
+
+int launch_t320(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
+  const int tm = a->M / 320, tn = a->N / 256;
+  hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_RESID>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A, a->lda,
+                     (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep);
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+int g_gemm_t320 = 0;  // echo_gemm_set_diag key 7: 320-row tiles in the auto pick: 0 = when they fill whole
+                      // rounds of the CUs, 1 = never, 2 = whenever at least one round (A/B)
 int g_gemm_stagger = 0;  // echo_gemm_set_diag key 1
 int g_gemm_no_rowsplit = 0;  // key 3: no row-tail split of 256x256 launches (A/B)
 int g_gemm_no_ps = 0;        // key 4: the 2-phase kernel instead of the persistent one (A/B)
@@ -1632,6 +1855,7 @@ extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   else if (key == 4) g_gemm_no_ps = value != 0;
   else if (key == 5) g_gemm_fill_min = value;
   else if (key == 6) g_gemm_ps_grid = value;
+  else if (key == 7) { if (value > 2) return ECHO_EINVAL; g_gemm_t320 = value; }
   else return ECHO_EINVAL;
   return 0;
 }
@@ -1706,6 +1930,13 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   }
   if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
   if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C) & 15) return ECHO_EALIGN;
+  // N = 2048 gated residual at M = 320 k: 320-row tiles when they fill whole rounds of the CUs (the 256x256
+  // tile count would leave a partial round); tile 20 forces them (bitwise equal either way)
+  if (a->tile == 20) return t320_ok(a) ? launch_t320(a, ep, s) : ECHO_EINVAL;
+  if (a->tile == 0 && g_gemm_t320 != 1 && t320_ok(a)) {
+    const int n320 = (a->M / 320) * (a->N / 256), cus = cu_count_cached();
+    if (g_gemm_t320 == 2 ? n320 >= cus : n320 % cus == 0) return launch_t320(a, ep, s);
+  }
   int tail_cfg = 0;
   const int M1 = (a->tile == 0 && (t == 13 || t == 16) && a->batch == 1 && !headnorm && !g_gemm_no_rowsplit)
                      ? split_rows(a->M, a->N, &tail_cfg) : 0;

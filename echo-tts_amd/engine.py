@@ -25,11 +25,15 @@ from .model import EchoDiTHip, KVStore, Workspace, prefix_lengths
 INIT_SCALE = 0.999  # inference.py:470
 
 # Batches of at least this many latent tokens (B x N, B even) run as two half-batch plans replayed
-# concurrently on two HIP streams (`StreamSplit`); 0 disables, ECHO_STREAM_SPLIT_MIN_TOKENS overrides.
-# Measured (tools/bench_streams.py, bench.py A/B on one box; rows bitwise equal either way):
-#   C3, 16 x 640: 2 x 8 prompts 2041 ms vs 2071 ms per call (+1.5 %); 4 x 4 prompts 3.6 % slower;
+# concurrently on two HIP streams (`StreamSplit`); 0 (the default) disables, ECHO_STREAM_SPLIT_MIN_TOKENS
+# sets it. Measured (bench.py A/B on one box; rows bitwise equal either way):
+#   round 2, C3 16 x 640: 2 x 8 prompts 2041 ms vs 2071 ms per call (+1.5 %; the other stream filled the
+#   partial last tile round of the N = 2048 residual GEMMs); 4 x 4 prompts 3.6 % slower;
+#   round 3, with 320-row residual tiles (whole rounds at M = 30720 / 10240, none at the half batch's
+#   15360): one stream 1987 / 1994 ms vs two streams 2015 / 2019 ms (one stream +1.3 %,
+#   profiles/r3_stream_split_ab.txt);
 #   C5, 16 x 160-latent blocks: 2 x 8 is 6.4 % slower (M = 3840 per launch is too small to fill the chip).
-STREAM_SPLIT_MIN_TOKENS = int(os.environ.get("ECHO_STREAM_SPLIT_MIN_TOKENS", str(16 * 640)))
+STREAM_SPLIT_MIN_TOKENS = int(os.environ.get("ECHO_STREAM_SPLIT_MIN_TOKENS", "0"))
 
 
 @dataclass(frozen=True)

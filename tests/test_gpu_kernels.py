@@ -177,6 +177,32 @@ def test_gemm_persistent_bias_bitwise(M, N, K):
     close_bf16(outs[0][:, :N], ref.cpu().float())
 
 
+@pytest.mark.parametrize("M,N,K", [(30720, 2048, 2048), (10240, 2048, 5888), (640, 512, 128), (960, 768, 192)])
+def test_gemm_t320_bitwise(M, N, K):
+    """320x256 tiles (tile 20; the auto pick for the N = 2048 gated residual when they fill whole rounds):
+    same per-element K order as the 256x256 kernels, so bitwise equal to the 2-phase kernel (tile 13) and to
+    the auto pick, with and without gate, in place on a column slice of a wider buffer (padding untouched);
+    close to an fp32 reference."""
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    g = torch.tanh(torch.randn(N, device=DEV)).to(BF)
+    h = torch.randn(M, N + 256, device=DEV).to(BF)
+    for gate in (g, None):
+        outs = []
+        for tile in (13, 20, 0):
+            buf = h.clone()
+            ops.gemm(a, w, out=buf[:, :N], epilogue=L.EPI_RESID, aux=buf[:, :N], gate=gate, tile=tile)
+            assert torch.equal(buf[:, N:], h[:, N:])
+            outs.append(buf)
+        assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    if M <= 1000:
+        y = rb(ref_linear(a, w))
+        ref = rb(h[:, :N].float().cpu() + rb(g.float().cpu() * y))
+        b = h.clone()
+        ops.gemm(a, w, out=b[:, :N], epilogue=L.EPI_RESID, aux=b[:, :N], gate=g, tile=20)
+        close_bf16(b[:, :N], ref)
+
+
 @pytest.mark.parametrize("epi", [L.EPI_STORE, L.EPI_RESID, L.EPI_F32OUT])
 def test_gemm_row_split_bitwise(epi):
     """Auto-tiled 10240x2048 launches split rows into whole 256x256 rounds + a smaller-tile tail;
