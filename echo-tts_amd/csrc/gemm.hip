@@ -1222,7 +1222,8 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
 }
 
 // ----------------------------------------------------------------------------- 320 x 256 tile
-// gemm_bf16_t320_kernel<EK_RESID>: 320x256x64 tiles for the N = 2048 gated-residual GEMMs (Wo, W2), whose
+// gemm_bf16_t320_kernel<EK_RESID | EK_SWIGLU>: 320x256x64 tiles for the N = 2048 gated-residual GEMMs (Wo, W2)
+// and W13 at M = 10240 (SwiGLU: 5.75 rounds of 320-row tiles vs 7.2 of 256-row ones), whose
 // 256x256 tile count leaves a partial last round at the decoder's M (M = 30720: 960 tiles = 3.75 rounds of
 // 256 CUs, M = 10240: 1.25 rounds) while 320-row tiles divide it exactly (768 / 256 tiles = 3 / 1 rounds).
 // Same fragments, MFMA and per-element K order as the 256x256 kernels: bitwise-equal results, so the
@@ -1239,7 +1240,7 @@ template <int EK>
 __global__ void __launch_bounds__(512)
 gemm_bf16_t320_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw,
                       void* __restrict__ Cv, int64_t ldc, int M, int N, int K, int tiles_m, int tiles_n, Epi ep) {
-  static_assert(EK == EK_RESID, "320-row tiles: gated residual epilogue");
+  static_assert(EK == EK_RESID || EK == EK_SWIGLU, "320-row tiles: gated residual or SwiGLU epilogue");
   constexpr int BM = 320, BN = 256, TM = 80, TN = 128, FM = 5, FN = 8;
   constexpr int STAGE = (BM + BN) * BK;
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
@@ -1366,13 +1367,39 @@ gemm_bf16_t320_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* _
   const int cpos = (g4 & 1) * 16 + (g4 >> 1) * 8;
   const int mb = m0 + wm * TM + (lane & 15);
   const int nb = n0 + wn * TN + cpos;
-  const __amdgpu_buffer_rsrc_t crs = brsrc(Cv, (uint32_t)(((int64_t)(M - 1) * ldc + N) * 2));
-  const __amdgpu_buffer_rsrc_t ars = brsrc(ep.aux, (uint32_t)(((int64_t)(M - 1) * ep.ld_aux + N) * 2));
+  const __amdgpu_buffer_rsrc_t crs =
+      brsrc(Cv, (uint32_t)(((int64_t)(M - 1) * ldc + (EK == EK_SWIGLU ? N / 2 : N)) * 2));
   auto swap_pair = [&](uint2 lo, uint2 hi) __attribute__((always_inline)) -> u32x4 {
     const auto s0 = __builtin_amdgcn_permlane16_swap(lo.x, hi.x, false, false);
     const auto s1 = __builtin_amdgcn_permlane16_swap(lo.y, hi.y, false, false);
     return u32x4{s0[0], s1[0], s0[1], s1[1]};
   };
+  if constexpr (EK == EK_SWIGLU) {
+    // gate / up column blocks interleaved by 16 (fragment 2jo gate, 2jo+1 up of output fragment jo): the
+    // persistent kernel's SwiGLU kind; output fragments (2p, 2p+1) form the swapped pair of 8 columns
+    const int nbo = n0 / 2 + wn * (TN / 2) + cpos;
+#pragma unroll
+    for (int ii = 0; ii < FM; ++ii) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        uint2 q[2];
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          float u[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float a = rbf(acc[ii][4 * p + 2 * jj][r]), b = rbf(acc[ii][4 * p + 2 * jj + 1][r]);
+            u[r] = rbf(silu_bf16in(a)) * b;
+          }
+          q[jj] = make_uint2(pack2bf(u[0], u[1]), pack2bf(u[2], u[3]));
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(swap_pair(q[0], q[1]), crs,
+                                               (uint32_t)(((mb + ii * 16) * ldc + nbo + p * 32) * 2), 0, 0);
+      }
+    }
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t ars = brsrc(ep.aux, (uint32_t)(((int64_t)(M - 1) * ep.ld_aux + N) * 2));
   u32x4 gv[FN / 2];
   if (ep.gate) {
 #pragma unroll
@@ -1819,28 +1846,47 @@ int cu_count_cached() {
   return g_num_cus;
 }
 
-// 320x256 tiles (gemm_bf16_t320_kernel): gated residual, M % 320 == 0, 32-bit buffer offsets, 16-B aligned
+// 320x256 tiles (gemm_bf16_t320_kernel): gated residual or SwiGLU, M % 320 == 0, 32-bit buffer offsets,
+// 16-B aligned operands
 bool t320_ok(const EchoGemmArgs* a) {
-  if (a->dtype != ECHO_BF16 || ek_of(a) != EK_RESID || a->batch != 1 || a->conv_taps > 0) return false;
+  const int ek = ek_of(a);
+  if (a->dtype != ECHO_BF16 || (ek != EK_RESID && ek != EK_SWIGLU) || a->batch != 1 || a->conv_taps > 0) return false;
   if (a->M % 320 || a->N % 256 || a->K % 64 || a->K < 128) return false;
   const int64_t lim = (int64_t)1 << 30;
-  if ((int64_t)a->M * a->ldc >= lim || (int64_t)a->M * a->ld_aux >= lim || (int64_t)a->M * a->lda >= lim ||
-      (int64_t)a->N * a->ldw >= lim)
+  if ((int64_t)a->M * a->ldc >= lim || (int64_t)a->M * a->lda >= lim || (int64_t)a->N * a->ldw >= lim) return false;
+  if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C) & 15) return false;
+  if (a->lda % 8 || a->ldw % 8 || a->ldc % 8) return false;
+  if (ek == EK_RESID &&
+      ((int64_t)a->M * a->ld_aux >= lim || a->ld_aux % 8 || (((uintptr_t)a->aux | (uintptr_t)a->gate) & 15)))
     return false;
-  if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C | (uintptr_t)a->aux | (uintptr_t)a->gate) & 15) return false;
-  return a->lda % 8 == 0 && a->ldw % 8 == 0 && a->ldc % 8 == 0 && a->ld_aux % 8 == 0;
+  return true;
 }
 
 int launch_t320(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   const int tm = a->M / 320, tn = a->N / 256;
-  hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_RESID>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A, a->lda,
-                     (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep);
+  if (ek_of(a) == EK_SWIGLU)
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_SWIGLU>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A,
+                       a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep);
+  else
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_RESID>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A,
+                       a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep);
   ECHO_LAUNCH_CHECK();
   return 0;
 }
 
-int g_gemm_t320 = 0;  // echo_gemm_set_diag key 7: 320-row tiles in the auto pick: 0 = when they fill whole
-                      // rounds of the CUs, 1 = never, 2 = whenever at least one round (A/B)
+// auto pick between 320x256 and 256x256 tiles by whole rounds of the CUs: 320-row tiles do 1.25x the work
+// per tile, so they win when they need fewer tile-rounds x 1.25 (N = 2048 residual at M = 30720: 3 x 1.25 vs
+// 4; M = 10240: 1 x 1.25 vs 2; W13 at M = 10240: 6 x 1.25 vs 8; not W13 at M = 30720: 18 x 1.25 vs 22)
+bool t320_pays(const EchoGemmArgs* a, int cus) {
+  const int64_t n320 = (int64_t)(a->M / 320) * (a->N / 256);
+  const int64_t n256 = (int64_t)((a->M + 255) / 256) * (a->N / 256);
+  if (n320 < cus) return false;
+  const double r320 = (double)((n320 + cus - 1) / cus) * 1.25, r256 = (double)((n256 + cus - 1) / cus);
+  return r320 < 0.98 * r256;
+}
+
+int g_gemm_t320 = 0;  // echo_gemm_set_diag key 7: 320-row tiles in the auto pick: 0 = when they need fewer
+                      // tile-rounds x 1.25 (t320_pays), 1 = never, 2 = whenever at least one round (A/B)
 int g_gemm_stagger = 0;  // echo_gemm_set_diag key 1
 int g_gemm_no_rowsplit = 0;  // key 3: no row-tail split of 256x256 launches (A/B)
 int g_gemm_no_ps = 0;        // key 4: the 2-phase kernel instead of the persistent one (A/B)
@@ -1930,12 +1976,12 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   }
   if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
   if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C) & 15) return ECHO_EALIGN;
-  // N = 2048 gated residual at M = 320 k: 320-row tiles when they fill whole rounds of the CUs (the 256x256
-  // tile count would leave a partial round); tile 20 forces them (bitwise equal either way)
+  // gated residual / SwiGLU at M = 320 k: 320-row tiles when they need fewer 1.25x tile-rounds than 256x256
+  // tiles (t320_pays); tile 20 forces them (bitwise equal either way)
   if (a->tile == 20) return t320_ok(a) ? launch_t320(a, ep, s) : ECHO_EINVAL;
   if (a->tile == 0 && g_gemm_t320 != 1 && t320_ok(a)) {
     const int n320 = (a->M / 320) * (a->N / 256), cus = cu_count_cached();
-    if (g_gemm_t320 == 2 ? n320 >= cus : n320 % cus == 0) return launch_t320(a, ep, s);
+    if (g_gemm_t320 == 2 ? n320 >= cus : t320_pays(a, cus)) return launch_t320(a, ep, s);
   }
   int tail_cfg = 0;
   const int M1 = (a->tile == 0 && (t == 13 || t == 16) && a->batch == 1 && !headnorm && !g_gemm_no_rowsplit)

@@ -203,6 +203,22 @@ def test_gemm_t320_bitwise(M, N, K):
         close_bf16(b[:, :N], ref)
 
 
+@pytest.mark.parametrize("M,N,K", [(10240, 11776, 2048), (640, 512, 128), (960, 768, 192)])
+def test_gemm_t320_swiglu_bitwise(M, N, K):
+    """320x256 tiles with the SwiGLU epilogue (the auto pick for W13 at M = 10240): bitwise equal to the
+    2-phase kernel and the auto pick; output a column slice of a wider buffer (padding untouched)."""
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    h = torch.randn(M, N // 2 + 256, device=DEV).to(BF)
+    outs = []
+    for tile in (13, 20, 0):
+        buf = h.clone()
+        ops.gemm(a, w, out=buf[:, :N // 2], epilogue=L.EPI_SWIGLU, tile=tile)
+        assert torch.equal(buf[:, N // 2:], h[:, N // 2:])
+        outs.append(buf)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
 @pytest.mark.parametrize("epi", [L.EPI_STORE, L.EPI_RESID, L.EPI_F32OUT])
 def test_gemm_row_split_bitwise(epi):
     """Auto-tiled 10240x2048 launches split rows into whole 256x256 rounds + a smaller-tile tail;
