@@ -1236,7 +1236,7 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
 // cW1 of tile k+1 in phase 0 of tile k: gemm_bf16_pp2_kernel's schedule and barrier argument with
 // c0-c2 -> cA + cW0 and c3 -> cW1, so the steady-state waits are vmcnt(9) (2 + 7 younger pieces).
 // Epilogue from registers, row fragment by row fragment (the residual rows of the next one in flight).
-template <int EK>
+template <int EK, int SP = 1>
 __global__ void __launch_bounds__(512)
 gemm_bf16_t320_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw,
                       void* __restrict__ Cv, int64_t ldc, int M, int N, int K, int tiles_m, int tiles_n, Epi ep) {
@@ -1294,11 +1294,16 @@ gemm_bf16_t320_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* _
   };
 
   const int nk = K / BK;
-  // prologue: tile 0 (cA, cW0, then cW1) and cA + cW0 of tile 1; wait for tile 0's cA + cW0
+  // SP = 1 (tile 21, A/B): DMA balanced between the two L segments — phase 0 of tile k issues cW0 and cW1 of
+  // tile k+1 (4 pieces), phase 1 cA of tile k+2 (5) instead of 2 / 7; cW0 then has one phase of DMA latency
+  // instead of two. Waits: phase 0 retires cW1(k) -> vmcnt(9) (cA(k+1) 5 + this phase's 4 younger), phase 1
+  // retires cA(k+1) + cW0(k+1) -> vmcnt(7). Measured within +-1 % of the 2 / 7 schedule on every decoder
+  // shape (profiles/r3_gemm_t320_dma_balance.txt): SP = 0 stays the default.
+  // prologue: tile 0 (cA, cW0, then cW1) and cA (SP) or cA + cW0 (!SP) of tile 1; wait for tile 0's cA + cW0
   dma(0, 0); dma(1, 0); dma(2, 0);
   if (nk > 1) {
-    dma(0, 1); dma(1, 1);
-    vm_wait_n<9>();
+    dma(0, 1);
+    if constexpr (SP) { vm_wait_n<7>(); } else { dma(1, 1); vm_wait_n<9>(); }
   } else {
     vm_wait_n<2>();
   }
@@ -1333,14 +1338,26 @@ gemm_bf16_t320_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* _
         for (int s = 0; s < 2; ++s)
           bfr[j][s] = *(const bf16x8*)(Bs + (wn * TN + ph * 64 + j * 16 + frow) * BK +
                                        (((4 * s + (lane >> 4)) ^ fsw) * 8));
-      if (ph == 0) {
-        if (n1) dma(2, kt + 1);
-        // retire cW1 of tile kt (issued in phase 0 of tile kt-1 / the prologue)
-        if (n1) vm_wait_n<9>(); else vm_wait_n<0>();
+      if constexpr (SP) {
+        if (ph == 0) {
+          if (n1) { dma(1, kt + 1); dma(2, kt + 1); }
+          // retire cW1 of tile kt (issued in phase 0 of tile kt-1 / the prologue)
+          if (n1) vm_wait_n<9>(); else vm_wait_n<0>();
+        } else {
+          if (n2) dma(0, kt + 2);
+          // retire cA + cW0 of tile kt+1
+          if (n2) vm_wait_n<7>(); else if (n1) vm_wait_n<2>(); else vm_wait_n<0>();
+        }
       } else {
-        if (n2) { dma(0, kt + 2); dma(1, kt + 2); }
-        // retire cA + cW0 of tile kt+1
-        if (n2) vm_wait_n<9>(); else if (n1) vm_wait_n<2>(); else vm_wait_n<0>();
+        if (ph == 0) {
+          if (n1) dma(2, kt + 1);
+          // retire cW1 of tile kt (issued in phase 0 of tile kt-1 / the prologue)
+          if (n1) vm_wait_n<9>(); else vm_wait_n<0>();
+        } else {
+          if (n2) { dma(0, kt + 2); dma(1, kt + 2); }
+          // retire cA + cW0 of tile kt+1
+          if (n2) vm_wait_n<9>(); else if (n1) vm_wait_n<2>(); else vm_wait_n<0>();
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       pp_barrier();
@@ -1862,17 +1879,19 @@ bool t320_ok(const EchoGemmArgs* a) {
   return true;
 }
 
-int launch_t320(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
+template <int SP>
+int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   const int tm = a->M / 320, tn = a->N / 256;
   if (ek_of(a) == EK_SWIGLU)
-    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_SWIGLU>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A,
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_SWIGLU, SP>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A,
                        a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep);
   else
-    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_RESID>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A,
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_RESID, SP>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A,
                        a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep);
   ECHO_LAUNCH_CHECK();
   return 0;
 }
+int launch_t320(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) { return launch_t320_sp<0>(a, ep, s); }
 
 // auto pick between 320x256 and 256x256 tiles by whole rounds of the CUs: 320-row tiles do 1.25x the work
 // per tile, so they win when they need fewer tile-rounds x 1.25 (N = 2048 residual at M = 30720: 3 x 1.25 vs
@@ -1979,6 +1998,7 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   // gated residual / SwiGLU at M = 320 k: 320-row tiles when they need fewer 1.25x tile-rounds than 256x256
   // tiles (t320_pays); tile 20 forces them (bitwise equal either way)
   if (a->tile == 20) return t320_ok(a) ? launch_t320(a, ep, s) : ECHO_EINVAL;
+  if (a->tile == 21) return t320_ok(a) ? launch_t320_sp<1>(a, ep, s) : ECHO_EINVAL;  // 4 / 5 DMA split (A/B)
   if (a->tile == 0 && g_gemm_t320 != 1 && t320_ok(a)) {
     const int n320 = (a->M / 320) * (a->N / 256), cus = cu_count_cached();
     if (g_gemm_t320 == 2 ? n320 >= cus : t320_pays(a, cus)) return launch_t320(a, ep, s);
