@@ -792,6 +792,10 @@ __global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_num_vgpr(96)))
   float m_run = -INFINITY, l_run = 0.f;
   const float sl2 = a.scale * 1.4426950408889634f;
   const int hb = 4 * h2;
+  // waves whose 32 queries all lie past n_q (the last q block of a 160-query blockwise launch has one
+  // active wave of four) issue their DMA share and take the barriers but skip every tile body (a scalar
+  // branch around opaque asm: the active waves' code is unchanged)
+  const bool wact = q0 + w * 32 < a.n_q;
   // prefix mask of the next tile (cursor mc advanced to it) if it is partial
   auto mask_tile = [&](auto par) __attribute__((always_inline)) {
     constexpr int P = decltype(par)::value;
@@ -823,11 +827,15 @@ __global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_num_vgpr(96)))
   for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   if (ntiles > 0) {
-    pl_qk_0(qf, ka);
-    mask_tile(std::integral_constant<int, 0>{});
-    float mx, ma;
-    pl_max_0(mx, ma);
-    decide(mx);
+    if (wact) {
+      pl_qk_0(qf, ka);
+      mask_tile(std::integral_constant<int, 0>{});
+      float mx, ma;
+      pl_max_0(mx, ma);
+      decide(mx);
+    } else {
+      advance(mc);
+    }
   }
   asm volatile("s_barrier" ::: "memory");  // every wave's K(0) reads are done: slot 0 takes K(2)
 
@@ -837,7 +845,9 @@ __global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_num_vgpr(96)))
     if (t + 1 < ntiles && !(ABL & 1)) dma_part(vc, 1, 1 - P);  // V(t+1) -> V slot (t+1) & 1 (V(t-1) was read in Y(t-1))
     const float msc = m_run == -INFINITY ? 0.f : -m_run * sl2;
     float ps;
-    if (t + 1 < ntiles) {
+    if (!wact) {
+      if (t + 1 < ntiles) advance(mc);
+    } else if (t + 1 < ntiles) {
       ps = 0.f;
       if constexpr (!(ABL & 2)) { if constexpr (P == 0) pl_x_0(qf, ka, sl2, msc, ps); else pl_x_1(qf, ka, sl2, msc, ps); }
       l_run += ps;

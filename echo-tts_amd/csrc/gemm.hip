@@ -1222,8 +1222,9 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
 }
 
 // ----------------------------------------------------------------------------- 320 x 256 tile
-// gemm_bf16_t320_kernel<EK_RESID | EK_SWIGLU>: 320x256x64 tiles for the N = 2048 gated-residual GEMMs (Wo, W2)
-// and W13 at M = 10240 (SwiGLU: 5.75 rounds of 320-row tiles vs 7.2 of 256-row ones), whose
+// gemm_bf16_t320_kernel<EK_RESID | EK_SWIGLU | EK_HEADNORM>: 320x256x64 tiles for the N = 2048 gated-residual
+// GEMMs (Wo, W2), W13 at M = 10240 (SwiGLU: 5.75 rounds of 320-row tiles vs 7.2 of 256-row ones) and the
+// blockwise QKVG launches (M = 2560 / 7680: 1 / 3 rounds instead of 1.25 / 3.75), whose
 // 256x256 tile count leaves a partial last round at the decoder's M (M = 30720: 960 tiles = 3.75 rounds of
 // 256 CUs, M = 10240: 1.25 rounds) while 320-row tiles divide it exactly (768 / 256 tiles = 3 / 1 rounds).
 // Same fragments, MFMA and per-element K order as the 256x256 kernels: bitwise-equal results, so the
@@ -1240,7 +1241,7 @@ template <int EK, int SP = 1>
 __global__ void __launch_bounds__(512)
 gemm_bf16_t320_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw,
                       void* __restrict__ Cv, int64_t ldc, int M, int N, int K, int tiles_m, int tiles_n, Epi ep) {
-  static_assert(EK == EK_RESID || EK == EK_SWIGLU, "320-row tiles: gated residual or SwiGLU epilogue");
+  static_assert(EK == EK_RESID || EK == EK_SWIGLU || EK == EK_HEADNORM, "320-row tiles: residual / SwiGLU / head norm");
   constexpr int BM = 320, BN = 256, TM = 80, TN = 128, FM = 5, FN = 8;
   constexpr int STAGE = (BM + BN) * BK;
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
@@ -1391,6 +1392,90 @@ gemm_bf16_t320_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* _
     const auto s1 = __builtin_amdgcn_permlane16_swap(lo.y, hi.y, false, false);
     return u32x4{s0[0], s1[0], s0[1], s1[1]};
   };
+  if constexpr (EK == EK_HEADNORM) {
+    // q/k RMSNorm + half RoPE (ECHO_EPI_HEADNORM), bitwise equal to the persistent kernel's HEADNORM kind
+    // and to echo_head_norm_rope: v = bf16(acc); per 8-column chunk c of the head the sum of squares in
+    // column order from 0; then the butterfly's tree over chunks (c ^ 8, c ^ 4, c ^ 2, c ^ 1); r = 1 /
+    // sqrtf(ss / 128 + eps); v = bf16(v * r * w); RoPE on column pairs in fp32; one rounding at the store.
+    // Here a wave's 128 columns are one whole head: chunk 2j + (g >> 1) of column fragment j (g = lane >> 4),
+    // its columns 0-3 in lanes g = 0, 2 and 4-7 in g = 1, 3 (one lane ^ 16 exchange); c ^ 8 is fragment
+    // j ^ 4 and c ^ 4, c ^ 2 fragments j ^ 2, j ^ 1 of the same lane; c ^ 1 is lane ^ 32.
+    const int hidx = (n0 + wn * TN) >> 7;
+    const int hblk = hidx / ep.hn_heads, hhd = hidx - hblk * ep.hn_heads;
+    const bool hnorm = hblk < ep.hn_nblk, hrope = hnorm && hhd < ep.hn_rope_heads;
+    const bool hi16 = (g4 & 1) != 0;
+    auto unpack = [](uint2 u, float (&v)[4]) __attribute__((always_inline)) {
+      v[0] = bf2f(u.x & 0xffffu); v[1] = bf2f(u.x >> 16); v[2] = bf2f(u.y & 0xffffu); v[3] = bf2f(u.y >> 16);
+    };
+    uint2 hw[FN];
+    if (hnorm) {
+      const bf16_t* wp = (const bf16_t*)ep.hn_w + hblk * ep.hn_w_stride + hhd * 128 + 4 * g4;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) hw[j] = *(const uint2*)(wp + j * 16);
+    }
+#pragma unroll
+    for (int ii = 0; ii < FM; ++ii) {
+      const int m = mb + ii * 16;
+      float4 rc[FN];
+      if (hrope) {  // (cos, sin) of the lane's 2 column pairs per fragment, in flight during the sums
+        const int pos = ep.hn_pos0 + ep.hn_pos_mult * (min(m, M - 1) % ep.hn_seq_len);
+        const float* rp = ep.hn_rope + ((int64_t)pos * 64 + 2 * g4) * 2;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) rc[j] = *(const float4*)(rp + j * 16);
+      }
+      uint2 hp[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        hp[j] = make_uint2(pack2bf(acc[ii][j][0], acc[ii][j][1]), pack2bf(acc[ii][j][2], acc[ii][j][3]));
+      if (hnorm) {
+        float c8[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          float v[4];
+          unpack(hp[j], v);
+          float h = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) h += v[e] * v[e];   // columns 0-3 (lanes g = 0, 2)
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(h), __float_as_uint(h), false, false);
+          float c = __uint_as_float(hi16 ? sw[0] : sw[1]);  // lane ^ 16's partial
+#pragma unroll
+          for (int e = 0; e < 4; ++e) c += v[e] * v[e];  // columns 4-7: the chunk's sum (lanes g = 1, 3)
+          c8[j] = c;
+        }
+        const float t3 = ((c8[0] + c8[4]) + (c8[2] + c8[6])) + ((c8[1] + c8[5]) + (c8[3] + c8[7]));
+        const auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(t3), __float_as_uint(t3), false, false);
+        const float t4 = t3 + __uint_as_float(lane >= 32 ? s32[0] : s32[1]);   // c ^ 1 (lane ^ 32)
+        const float r = 1.0f / sqrtf(t4 / 128.0f + ep.hn_eps);
+        const auto sr = __builtin_amdgcn_permlane16_swap(__float_as_uint(r), __float_as_uint(r), false, false);
+        const float rr = hi16 ? r : __uint_as_float(sr[1]);  // lanes g = 0, 2 take lane ^ 16's
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          float v[4], wv[4];
+          unpack(hp[j], v);
+          unpack(hw[j], wv);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (v[e] * rr) * wv[e];
+          hp[j] = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));   // bf16(v * r * w)
+        }
+        if (hrope) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            float v[4];
+            unpack(hp[j], v);
+            const float4 cs = rc[j];
+            const float y0 = (v[0] * cs.x) - (v[1] * cs.y), y1 = (v[0] * cs.y) + (v[1] * cs.x);
+            const float y2 = (v[2] * cs.z) - (v[3] * cs.w), y3 = (v[2] * cs.w) + (v[3] * cs.z);
+            hp[j] = make_uint2(pack2bf(y0, y1), pack2bf(y2, y3));
+          }
+        }
+      }
+      const uint32_t off = (uint32_t)((m * ldc + nb) * 2);
+#pragma unroll
+      for (int p = 0; p < FN / 2; ++p)
+        __builtin_amdgcn_raw_buffer_store_b128(swap_pair(hp[2 * p], hp[2 * p + 1]), crs, off + p * 64, 0, 0);
+    }
+    return;
+  }
   if constexpr (EK == EK_SWIGLU) {
     // gate / up column blocks interleaved by 16 (fragment 2jo gate, 2jo+1 up of output fragment jo): the
     // persistent kernel's SwiGLU kind; output fragments (2p, 2p+1) form the swapped pair of 8 columns
@@ -1863,11 +1948,14 @@ int cu_count_cached() {
   return g_num_cus;
 }
 
-// 320x256 tiles (gemm_bf16_t320_kernel): gated residual or SwiGLU, M % 320 == 0, 32-bit buffer offsets,
+// 320x256 tiles (gemm_bf16_t320_kernel): gated residual, SwiGLU or head norm, M % 320 == 0, 32-bit buffer offsets,
 // 16-B aligned operands
 bool t320_ok(const EchoGemmArgs* a) {
   const int ek = ek_of(a);
-  if (a->dtype != ECHO_BF16 || (ek != EK_RESID && ek != EK_SWIGLU) || a->batch != 1 || a->conv_taps > 0) return false;
+  if (a->dtype != ECHO_BF16 || (ek != EK_RESID && ek != EK_SWIGLU && ek != EK_HEADNORM) || a->batch != 1 ||
+      a->conv_taps > 0)
+    return false;
+  if (ek == EK_HEADNORM && a->hn_heads <= 0) return false;
   if (a->M % 320 || a->N % 256 || a->K % 64 || a->K < 128) return false;
   const int64_t lim = (int64_t)1 << 30;
   if ((int64_t)a->M * a->ldc >= lim || (int64_t)a->M * a->lda >= lim || (int64_t)a->N * a->ldw >= lim) return false;
@@ -1885,6 +1973,9 @@ int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   if (ek_of(a) == EK_SWIGLU)
     hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_SWIGLU, SP>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A,
                        a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep);
+  else if (ek_of(a) == EK_HEADNORM)
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_HEADNORM, SP>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A,
+                       a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep);
   else
     hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_RESID, SP>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A,
                        a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep);
@@ -1893,19 +1984,22 @@ int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 }
 int launch_t320(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) { return launch_t320_sp<0>(a, ep, s); }
 
-// auto pick between 320x256 and 256x256 tiles by whole rounds of the CUs: 320-row tiles do 1.25x the work
-// per tile, so they win when they need fewer tile-rounds x 1.25 (N = 2048 residual at M = 30720: 3 x 1.25 vs
-// 4; M = 10240: 1 x 1.25 vs 2; W13 at M = 10240: 6 x 1.25 vs 8; not W13 at M = 30720: 18 x 1.25 vs 22)
+// auto pick between 320x256 and 256x256 tiles by whole rounds of the CUs: a 320-row tile does 1.25x the work
+// of a 256-row one in ≈1.2x the time (more MFMA per staged byte; HEADNORM: one wave per head, no LDS
+// exchange), so 320-row tiles win when ⌈tiles320 / CUs⌉ x 1.2 < ⌈tiles256 / CUs⌉ (tools/bench_gemm.py,
+// bench_qkvg.py): the N = 2048 residual at M = 30720 / 10240 (3.6 vs 4, 1.2 vs 2), W13 at M = 30720 / 10240
+// (21.6 vs 22, 7.2 vs 8), QKVG + head norm at M = 30720 / 10240 / 7680 / 2560 (14.4 vs 15, 4.8 vs 5,
+// 3.6 vs 4, 1.2 vs 2); not W13 at M = 7680 / 2560 (6 vs 6, 2.4 vs 2)
 bool t320_pays(const EchoGemmArgs* a, int cus) {
   const int64_t n320 = (int64_t)(a->M / 320) * (a->N / 256);
   const int64_t n256 = (int64_t)((a->M + 255) / 256) * (a->N / 256);
   if (n320 < cus) return false;
-  const double r320 = (double)((n320 + cus - 1) / cus) * 1.25, r256 = (double)((n256 + cus - 1) / cus);
-  return r320 < 0.98 * r256;
+  const double r320 = (double)((n320 + cus - 1) / cus) * 1.2, r256 = (double)((n256 + cus - 1) / cus);
+  return r320 < 0.99 * r256;
 }
 
 int g_gemm_t320 = 0;  // echo_gemm_set_diag key 7: 320-row tiles in the auto pick: 0 = when they need fewer
-                      // tile-rounds x 1.25 (t320_pays), 1 = never, 2 = whenever at least one round (A/B)
+                      // tile-rounds x 1.2 (t320_pays), 1 = never, 2 = whenever at least one round (A/B)
 int g_gemm_stagger = 0;  // echo_gemm_set_diag key 1
 int g_gemm_no_rowsplit = 0;  // key 3: no row-tail split of 256x256 launches (A/B)
 int g_gemm_no_ps = 0;        // key 4: the 2-phase kernel instead of the persistent one (A/B)
@@ -1966,7 +2060,8 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   if (a->tile == 0 && t == 1) t = (a->dtype == ECHO_BF16 && ps_ok(a, ek_of(a)) && !g_gemm_no_ps) ? 16 : 13;
   // fused on the persistent kernel (t 16/17/18, N % 256 == 0, via ps_ok) or the 2-phase one (t 13)
   const bool hn_fused = a->dtype == ECHO_BF16 && ((t == 13 && a->N % 128 == 0) ||
-                                                   ((t == 16 || t == 17 || t == 18) && ps_ok(a, EK_HEADNORM)));
+                                                   ((t == 16 || t == 17 || t == 18) && ps_ok(a, EK_HEADNORM)) ||
+                                                   ((t == 20 || t == 21) && t320_ok(a)));
   if (headnorm && !hn_fused) {
     // not fused for this shape / dtype: plain store, then the standalone kernel (same results)
     EchoGemmArgs b = *a;
@@ -1995,8 +2090,8 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   }
   if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
   if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C) & 15) return ECHO_EALIGN;
-  // gated residual / SwiGLU at M = 320 k: 320-row tiles when they need fewer 1.25x tile-rounds than 256x256
-  // tiles (t320_pays); tile 20 forces them (bitwise equal either way)
+  // gated residual / SwiGLU / head norm at M = 320 k: 320-row tiles when they need fewer 1.2x tile-rounds than
+  // 256x256 tiles (t320_pays); tile 20 forces them (bitwise equal either way)
   if (a->tile == 20) return t320_ok(a) ? launch_t320(a, ep, s) : ECHO_EINVAL;
   if (a->tile == 21) return t320_ok(a) ? launch_t320_sp<1>(a, ep, s) : ECHO_EINVAL;  // 4 / 5 DMA split (A/B)
   if (a->tile == 0 && g_gemm_t320 != 1 && t320_ok(a)) {

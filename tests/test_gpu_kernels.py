@@ -490,9 +490,9 @@ def _pipeline_case(case):
     empty text rows, a 1-tile item, a 1-query launch, segments shorter than a tile, spiky scores."""
     g = torch.Generator(device=DEV).manual_seed(11)
     rn = lambda *s: torch.randn(*s, device=DEV, generator=g)
-    if case in ("cfg640", "plain600"):
+    if case in ("cfg640", "plain600", "blk160", "blk200"):
         B, H, T, P = 4, 16, 448, 160
-        n_q, R = (640, 3 * B) if case == "cfg640" else (600, B)
+        n_q, R = {"cfg640": (640, 3 * B), "plain600": (600, B), "blk160": (160, 3 * B), "blk200": (200, B)}[case]
         qkvg, kt, ks = rn(R, n_q, 4, H, 128).to(BF), rn(B, T, 2, H, 128).to(BF), rn(B, P, 2, H, 128).to(BF)
         tl = torch.tensor(([388, 0, 201, 448] + [0] * B + [388, 0, 201, 448])[:R], dtype=torch.int32, device=DEV)
         sl = torch.tensor(([P] * 2 * B + [0] * B)[:R], dtype=torch.int32, device=DEV)
@@ -516,11 +516,12 @@ def _pipeline_case(case):
     raise ValueError(case)
 
 
-@pytest.mark.parametrize("case", ["cfg640", "plain600", "one_tile", "one_query", "spikes"])
+@pytest.mark.parametrize("case", ["cfg640", "plain600", "blk160", "blk200", "one_tile", "one_query", "spikes"])
 def test_attention_pipeline_bitwise(case):
     """The asm-owned software-pipelined kernel (attn_pl_kernel: production for non-causal launches,
     variant 11) computes attn_bf16_kernel<0, 4, 2>'s math in the same order: bitwise equal to variant 0,
-    through ops.attention and the variant entry, with and without a gate; close to fp64."""
+    through ops.attention and the variant entry, with and without a gate; close to fp64. blk160 / blk200:
+    last q blocks with 1 / 3 active waves (the others skip every tile body)."""
     q, segs, gate = _pipeline_case(case)
     R, n_q, H = q.shape[0], q.shape[1], q.shape[3]
     ref = torch.full((R, n_q, H, 128), float("nan"), device=DEV, dtype=BF)
@@ -772,6 +773,28 @@ def test_gemm_headnorm_fused(tile, M, H, pos0, rh, K):
     hn = ops.HeadNorm(nw, H, 2, 1e-5, w_stride=H * 128, rope=rope, rope_heads=rh, seq_len=seq, pos0=pos0)
     got = ops.gemm(a, w, tile=tile, head_norm=hn)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("M,H,pos0,rh,K", [(2560, 16, 0, 8, 2048), (7680, 16, 3, 8, 256), (640, 10, 0, 10, 128),
+                                          (960, 4, 5, 2, 256)])
+def test_gemm_headnorm_t320(M, H, pos0, rh, K):
+    """ECHO_EPI_HEADNORM on 320x256 tiles (tile 20; the auto pick for the blockwise QKVG launches, M = 2560 /
+    7680), where each wave holds one whole head: bitwise equal to store + echo_head_norm_rope and to the
+    2-phase kernel's fused epilogue; decoder (half RoPE) and encoder (full RoPE) layouts."""
+    from echo_tts_amd.model import rope_table_cpu
+    N = 4 * H * 128
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    nw = (1 + 0.1 * torch.randn(2, H, 128, device=DEV)).to(BF)
+    rope = rope_table_cpu(128, 4096).to(DEV)
+    seq = 160 if M % 160 == 0 else M
+    ref = ops.gemm(a, w, tile=13)
+    ops.head_norm_rope(ref, H, nw, 1e-5, nblk=2, col0=0, col_stride=H * 128, w_stride=H * 128, rope=rope,
+                       rope_heads=rh, seq_len=seq, pos0=pos0)
+    hn = ops.HeadNorm(nw, H, 2, 1e-5, w_stride=H * 128, rope=rope, rope_heads=rh, seq_len=seq, pos0=pos0)
+    for tile in (20, 21, 0, 13):
+        got = ops.gemm(a, w, tile=tile, head_norm=hn)
+        assert torch.equal(got, ref), tile
 
 
 def test_gemm_headnorm_rejects_bad_args():

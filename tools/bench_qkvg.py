@@ -1,5 +1,7 @@
 """QKVG projection of the decoder, two ways, interleaved in one process (HIP events):
-  fused      — auto tile: gemm_bf16_ps_kernel<HEADNORM> (persistent, register epilogue, round 3)
+  fused      — auto tile (t320_pays: 320x256 tiles where they need fewer tile-rounds, else the 256x256
+               persistent kernel's register epilogue)
+  fused_ps / fused_t320 — forced 256x256 persistent (tile 16) / 320x256 (tile 20)
   fused_pp2  — gemm_bf16_pp2_kernel<HEADNORM>: the 2-phase kernel's LDS-staged epilogue (tile 13)
   split      — persistent store GEMM (gemm_bf16_ps_kernel<STORE>) + head_norm_rope on the q/k blocks
 Both give bitwise-equal outputs (tests/test_gpu_kernels.py); this measures which is faster.
@@ -21,13 +23,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--ms", default="30720,10240", help="comma list of row counts (2560 / 7680: blockwise C5)")
     args = ap.parse_args()
     dev, D, H, N = "cuda", 2048, 16, 640
     torch.manual_seed(0)
     w = (torch.randn(4 * D, D, device=dev) * 0.02).to(torch.bfloat16)
     qk = (1 + 0.1 * torch.randn(2, H, 128, device=dev)).to(torch.bfloat16)
     rope = rope_table_cpu(128, MAX_POS).to(dev)
-    for M in (30720, 10240):
+    for M in (int(v) for v in args.ms.split(",")):
         x = torch.randn(M, D, device=dev).to(torch.bfloat16)
         out = torch.empty(M, 4 * D, device=dev, dtype=torch.bfloat16)
         hn = ops.HeadNorm(qk, H, 2, 1e-5, w_stride=H * 128, rope=rope, rope_heads=H // 2, seq_len=N, pos0=0)
@@ -37,6 +40,12 @@ def main():
 
         def fused_pp2():
             ops.gemm(x, w, out=out, head_norm=hn, tile=13)
+
+        def fused_t320():  # 320x256 tiles (tile 20; rows must be a multiple of 320)
+            ops.gemm(x, w, out=out, head_norm=hn, tile=20 if M % 320 == 0 else 0)
+
+        def fused_ps():  # the 256x256 persistent kernel (tile 16)
+            ops.gemm(x, w, out=out, head_norm=hn, tile=16)
 
         def split():
             ops.gemm(x, w, out=out)
@@ -55,8 +64,10 @@ def main():
         same = bool(torch.equal(a, out))
         fused_pp2()
         same = same and bool(torch.equal(a, out))
-        arms = (("fused", fused), ("fused_pp2", fused_pp2), ("split", split), ("store_ps", store_ps),
-                ("store_pp2", store_pp2))
+        fused_t320()
+        same = same and bool(torch.equal(a, out))
+        arms = (("fused", fused), ("fused_ps", fused_ps), ("fused_t320", fused_t320), ("fused_pp2", fused_pp2),
+                ("split", split), ("store_ps", store_ps), ("store_pp2", store_pp2))
         times = {k: [] for k, _ in arms}
         for _ in range(args.rounds):
             for name, fn in arms:
