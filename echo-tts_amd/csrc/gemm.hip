@@ -1998,11 +1998,31 @@ bool t320_pays(const EchoGemmArgs* a, int cus) {
   return r320 < 0.99 * r256;
 }
 
+// Column split of a 320-row launch whose tile count leaves a partial round (W13, N = 11776 = 46 tile
+// columns): the first c1 tile columns as whole rounds of 320x256 tiles, the other N - 256 c1 columns as a
+// second launch on the persistent 256x256 kernel (same K order per element: bitwise equal). Cost in
+// 256x256 tile-rounds (a 320-row round = 1.2); returns c1, or 0 when no split beats the best single launch
+// by 2 % (M = 30720: c1 = 40, 15 x 1.2 + 3 = 21 vs 21.6; M = 10240: 5 x 1.2 + 1 = 7 vs 7.2).
+int t320_col_split(const EchoGemmArgs* a, int cus) {
+  const int64_t pm = a->M / 320, p256 = (a->M + 255) / 256, tn = a->N / 256;
+  auto rounds = [&](int64_t tiles) { return (double)((tiles + cus - 1) / cus); };
+  const double one = std::min(pm * tn >= cus ? rounds(pm * tn) * 1.2 : 1e300, rounds(p256 * tn));
+  double best = 0.98 * one;
+  int c1 = 0;
+  for (int64_t c = 1; c < tn; ++c) {
+    if (pm * c < cus) continue;
+    const double e = rounds(pm * c) * 1.2 + rounds(p256 * (tn - c)) + 0.05;
+    if (e < best) { best = e; c1 = (int)c; }
+  }
+  return c1;
+}
+
 int g_gemm_t320 = 0;  // echo_gemm_set_diag key 7: 320-row tiles in the auto pick: 0 = when they need fewer
                       // tile-rounds x 1.2 (t320_pays), 1 = never, 2 = whenever at least one round (A/B)
 int g_gemm_stagger = 0;  // echo_gemm_set_diag key 1
 int g_gemm_no_rowsplit = 0;  // key 3: no row-tail split of 256x256 launches (A/B)
 int g_gemm_no_ps = 0;        // key 4: the 2-phase kernel instead of the persistent one (A/B)
+int g_gemm_no_colsplit = 0;  // key 8: no column split of 320-row launches (t320_col_split; A/B)
 
 }  // namespace
 
@@ -2015,6 +2035,7 @@ extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   else if (key == 5) g_gemm_fill_min = value;
   else if (key == 6) g_gemm_ps_grid = value;
   else if (key == 7) { if (value > 2) return ECHO_EINVAL; g_gemm_t320 = value; }
+  else if (key == 8) g_gemm_no_colsplit = value != 0;
   else return ECHO_EINVAL;
   return 0;
 }
@@ -2094,6 +2115,24 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   // 256x256 tiles (t320_pays); tile 20 forces them (bitwise equal either way)
   if (a->tile == 20) return t320_ok(a) ? launch_t320(a, ep, s) : ECHO_EINVAL;
   if (a->tile == 21) return t320_ok(a) ? launch_t320_sp<1>(a, ep, s) : ECHO_EINVAL;  // 4 / 5 DMA split (A/B)
+  if (a->tile == 0 && g_gemm_t320 == 0 && !g_gemm_no_colsplit && a->batch == 1 && !headnorm && t320_ok(a)) {
+    const int c1 = t320_col_split(a, cu_count_cached());
+    if (c1 > 0) {
+      // two launches on the same stream: tile columns [0, c1) on 320-row tiles, the rest by the auto pick
+      const int n1 = c1 * 256;
+      EchoGemmArgs h = *a, r = *a;
+      h.N = n1;
+      h.tile = 20;
+      r.N = a->N - n1;
+      r.W = (const bf16_t*)a->W + (int64_t)n1 * a->ldw;
+      r.C = (bf16_t*)a->C + (a->epilogue == ECHO_EPI_SWIGLU ? n1 / 2 : n1);
+      if (a->aux) r.aux = (const bf16_t*)a->aux + n1;
+      if (a->gate) r.gate = (const bf16_t*)a->gate + n1;
+      if (a->bias) r.bias = (const bf16_t*)a->bias + n1;
+      const int rc = echo_gemm(&h, stream);
+      return rc ? rc : echo_gemm(&r, stream);
+    }
+  }
   if (a->tile == 0 && g_gemm_t320 != 1 && t320_ok(a)) {
     const int n320 = (a->M / 320) * (a->N / 256), cus = cu_count_cached();
     if (g_gemm_t320 == 2 ? n320 >= cus : t320_pays(a, cus)) return launch_t320(a, ep, s);

@@ -94,8 +94,9 @@ int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch);
  * 256x256 launches; key 5: tile count below which an auto-picked 256x256 launch switches to a
  * smaller tile (default 128); key 6: cap on the persistent kernel's workgroup count (0 = one per CU);
  * key 7: 320x256 tiles for the gated residual / SwiGLU / head norm (0 = when they need fewer 1.2x
- * tile-rounds than 256x256 tiles, 1 = never, 2 = whenever they fill at least one round)
- * (A/B timing, tools/bench_streams.py --diag; all bitwise-equal). */
+ * tile-rounds than 256x256 tiles, 1 = never, 2 = whenever they fill at least one round); key 8: 1 = no
+ * column split of auto-picked 320-row launches (W13: 320-row tiles on whole rounds of tile columns, the
+ * rest on the persistent 256x256 kernel) (A/B timing, tools/bench_streams.py --diag; all bitwise-equal). */
 int echo_gemm_set_diag(int32_t key, int32_t value);
 
 /* One key/value segment of the joint attention (model.py:246-253): rows of

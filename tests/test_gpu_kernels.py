@@ -177,11 +177,12 @@ def test_gemm_persistent_bias_bitwise(M, N, K):
     close_bf16(outs[0][:, :N], ref.cpu().float())
 
 
-@pytest.mark.parametrize("M,N,K", [(30720, 2048, 2048), (10240, 2048, 5888), (640, 512, 128), (960, 768, 192)])
+@pytest.mark.parametrize("M,N,K", [(30720, 2048, 2048), (10240, 2048, 5888), (10240, 11776, 128), (640, 512, 128),
+                                   (960, 768, 192)])
 def test_gemm_t320_bitwise(M, N, K):
     """320x256 tiles (tile 20; the auto pick for the N = 2048 gated residual when they fill whole rounds):
     same per-element K order as the 256x256 kernels, so bitwise equal to the 2-phase kernel (tile 13) and to
-    the auto pick, with and without gate, in place on a column slice of a wider buffer (padding untouched);
+    the auto pick (N = 11776: column split, 320-row tiles on the first 40 tile columns), with and without gate, in place on a column slice of a wider buffer (padding untouched);
     close to an fp32 reference."""
     a = torch.randn(M, K, device=DEV).to(BF)
     w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
@@ -203,10 +204,11 @@ def test_gemm_t320_bitwise(M, N, K):
         close_bf16(b[:, :N], ref)
 
 
-@pytest.mark.parametrize("M,N,K", [(10240, 11776, 2048), (640, 512, 128), (960, 768, 192)])
+@pytest.mark.parametrize("M,N,K", [(10240, 11776, 2048), (30720, 11776, 256), (640, 512, 128), (960, 768, 192)])
 def test_gemm_t320_swiglu_bitwise(M, N, K):
-    """320x256 tiles with the SwiGLU epilogue (the auto pick for W13 at M = 10240): bitwise equal to the
-    2-phase kernel and the auto pick; output a column slice of a wider buffer (padding untouched)."""
+    """320x256 tiles with the SwiGLU epilogue (W13 at M = 30720 / 10240: the auto pick splits the columns,
+    320-row tiles on the first 40 tile columns, the persistent 256x256 kernel on the last 6): bitwise equal
+    to the 2-phase kernel and the auto pick; output a column slice of a wider buffer (padding untouched)."""
     a = torch.randn(M, K, device=DEV).to(BF)
     w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
     h = torch.randn(M, N // 2 + 256, device=DEV).to(BF)

@@ -4,6 +4,7 @@ Interleaved rounds of every tile config in one process (cdna_hip_programming.md 
 rule 24), random operands, HIP events on the launch stream. Also checks that each
 config's output is bitwise equal to config 1 (same K accumulation order).
     python tools/bench_gemm.py [--tiles 1,6] [--rounds 5]
+Tile -8: the auto pick with the column split of 320-row launches off (echo_gemm_set_diag key 8).
 """
 import argparse
 import os
@@ -26,6 +27,17 @@ SHAPES = [  # name, M, N, K, epilogue
     ("w13  M10240", 10240, 11776, 2048, L.EPI_SWIGLU),
     ("w2   M10240", 10240, 2048, 5888, L.EPI_RESID),
 ]
+
+
+def gemm_t(a, w, t, **kw):
+    """ops.gemm with tile t; t = -8: auto pick, column split of 320-row launches off"""
+    if t == -8:
+        L.load().echo_gemm_set_diag(8, 1)
+        try:
+            return ops.gemm(a, w, tile=0, **kw)
+        finally:
+            L.load().echo_gemm_set_diag(8, 0)
+    return ops.gemm(a, w, tile=t, **kw)
 
 
 def timeit_fill(out, args):
@@ -78,7 +90,7 @@ def main():
         for t in tiles:
             odt = torch.float32 if epi == L.EPI_F32OUT else torch.bfloat16
             o = aux.clone() if epi == L.EPI_RESID else torch.empty(M, nout, device=dev, dtype=odt)
-            ops.gemm(a, w, out=o, epilogue=epi, aux=o if epi == L.EPI_RESID else None, gate=gate, bias=bias, tile=t)
+            gemm_t(a, w, t, out=o, epilogue=epi, aux=o if epi == L.EPI_RESID else None, gate=gate, bias=bias)
             outs[t] = o
         base = outs[tiles[0]]
         same = {t: bool(torch.equal(outs[t], base)) for t in tiles}
@@ -90,8 +102,8 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(args.iters):
-                    ops.gemm(a, w, out=out, epilogue=epi, aux=aux if epi == L.EPI_RESID else None, gate=gate,
-                             bias=bias, tile=t)
+                    gemm_t(a, w, t, out=out, epilogue=epi, aux=aux if epi == L.EPI_RESID else None, gate=gate,
+                           bias=bias)
                 e1.record()
                 torch.cuda.synchronize()
                 times[t].append(e0.elapsed_time(e1) / args.iters)
