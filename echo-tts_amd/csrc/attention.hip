@@ -721,10 +721,12 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
 // ABL (timing ablations, variants 12-19; results wrong except 32): 1 no loop DMA, 2 no X body, 4 no Y body,
 // 8 no end-of-tile wait + barrier, 16 no tile loop; 32 (diagnostic, results right): CFG rows of one prompt
 // (r, r + B, r + 2B; B = segment 1's batch_mod) adjacent in the block order
-template <int ABL>
-__global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_num_vgpr(96)))
+// NW: waves per workgroup (4: 128 queries, two workgroups per CU; 8: 256 queries, one workgroup per CU, each
+// K/V tile staged once for twice the queries)
+template <int ABL, int NW = 4>
+__global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgpu_num_vgpr(96)))
     attn_pl_kernel(EchoAttnArgs a_arg) {
-  constexpr int NW = 4, QB = 128, DPT = 4, KTT = KT;
+  constexpr int QB = 32 * NW, DPT = 16 / NW, KTT = KT;
   __shared__ __attribute__((aligned(16))) bf16_t lds[4 * KT * 128];  // K slot 0, 1 | V slot 0, 1
 
   using KArgs = const __attribute__((address_space(4))) EchoAttnArgs;
@@ -1392,6 +1394,14 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 17: hipLaunchKernelGGL(attn_pl_kernel<6>, grid, dim3(256), 0, s, *a); break;
     case 18: hipLaunchKernelGGL(attn_pl_kernel<7>, grid, dim3(256), 0, s, *a); break;
     case 19: hipLaunchKernelGGL(attn_pl_kernel<32>, grid, dim3(256), 0, s, *a); break;
+    case 20: case 21: case 22: {  // asm pipeline at 8 waves x 32 queries (21: no tile loop, 22: no X / Y bodies)
+      if (any_causal(a)) return ECHO_EINVAL;
+      const dim3 g8(attn_grid(a, 256));
+      if (cfg == 20) hipLaunchKernelGGL((attn_pl_kernel<0, 8>), g8, dim3(512), 0, s, *a);
+      else if (cfg == 21) hipLaunchKernelGGL((attn_pl_kernel<16, 8>), g8, dim3(512), 0, s, *a);
+      else hipLaunchKernelGGL((attn_pl_kernel<6, 8>), g8, dim3(512), 0, s, *a);
+      break;
+    }
     default: return ECHO_EINVAL;
   }
 #undef ECHO_ATTN_ABLS
