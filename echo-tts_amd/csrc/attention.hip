@@ -741,7 +741,18 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
     const int B = a.nseg > 1 ? a.seg[1].batch_mod : a.rows;
     if (a.rows == 3 * B) row = (row % 3) * B + row / 3;
   }
-  const int head = Lr / a.rows;
+  int head = Lr / a.rows;
+  if constexpr ((ABL & 64) != 0) {
+    // diagnostic order (results right): each XCD's chunk holds heads/8 whole heads, rows slowest, the three
+    // CFG row groups in the order cond, uncond-speaker, uncond-text (longest first at C3's lengths)
+    if (a.heads % 8 == 0) {
+      const int chunk = gridDim.x >> 3, x = L / chunk, p = L - x * chunk, hpx = a.heads >> 3;
+      const int rest = p / nqb, slot = rest / hpx;
+      head = x * hpx + rest % hpx;
+      const int B = a.nseg > 1 ? a.seg[1].batch_mod : a.rows;
+      row = (a.rows == 3 * B) ? (slot < B ? slot : slot < 2 * B ? slot + B : slot - B) : slot;
+    }
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h2 = lane >> 5, ql = lane & 31;
@@ -1394,6 +1405,8 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 17: hipLaunchKernelGGL(attn_pl_kernel<6>, grid, dim3(256), 0, s, *a); break;
     case 18: hipLaunchKernelGGL(attn_pl_kernel<7>, grid, dim3(256), 0, s, *a); break;
     case 19: hipLaunchKernelGGL(attn_pl_kernel<32>, grid, dim3(256), 0, s, *a); break;
+    case 23: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<64>, grid, dim3(256), 0, s, *a); break;
+    case 24: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<32>, grid, dim3(256), 0, s, *a); break;
     case 20: case 21: case 22: {  // asm pipeline at 8 waves x 32 queries (21: no tile loop, 22: no X / Y bodies)
       if (any_causal(a)) return ECHO_EINVAL;
       const dim3 g8(attn_grid(a, 256));
