@@ -720,7 +720,8 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
 
 // ABL (timing ablations, variants 12-19; results wrong except 32): 1 no loop DMA, 2 no X body, 4 no Y body,
 // 8 no end-of-tile wait + barrier, 16 no tile loop; 32 (diagnostic, results right): CFG rows of one prompt
-// (r, r + B, r + 2B; B = segment 1's batch_mod) adjacent in the block order
+// (r, r + B, r + 2B; B = segment 1's batch_mod) adjacent in the block order; 64 (diagnostic, results right):
+// longest-first block order per XCD; 128 (results right): V(t+1)'s DMA between the X and Y bodies
 // NW: waves per workgroup (4: 128 queries, two workgroups per CU; 8: 256 queries, one workgroup per CU, each
 // K/V tile staged once for twice the queries)
 template <int ABL, int NW = 4>
@@ -855,16 +856,19 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
   auto iter = [&](int t, auto par) __attribute__((always_inline)) {
     constexpr int P = decltype(par)::value;
     if (t + 2 < ntiles && !(ABL & 1)) dma_part(kc, 0, P);      // K(t+2) -> K slot t & 1 (K(t) was read in X(t-1))
-    if (t + 1 < ntiles && !(ABL & 1)) dma_part(vc, 1, 1 - P);  // V(t+1) -> V slot (t+1) & 1 (V(t-1) was read in Y(t-1))
+    // V(t+1) -> V slot (t+1) & 1 (V(t-1) was read in Y(t-1)); ABL 128: issued between X(t) and Y(t) instead
+    if (!(ABL & 128) && t + 1 < ntiles && !(ABL & 1)) dma_part(vc, 1, 1 - P);
     const float msc = m_run == -INFINITY ? 0.f : -m_run * sl2;
     float ps;
     if (!wact) {
       if (t + 1 < ntiles) advance(mc);
+      if ((ABL & 128) && !(ABL & 1) && t + 1 < ntiles) dma_part(vc, 1, 1 - P);
     } else if (t + 1 < ntiles) {
       ps = 0.f;
       if constexpr (!(ABL & 2)) { if constexpr (P == 0) pl_x_0(qf, ka, sl2, msc, ps); else pl_x_1(qf, ka, sl2, msc, ps); }
       l_run += ps;
       mask_tile(std::integral_constant<int, 1 - P>{});
+      if ((ABL & 128) && !(ABL & 1)) dma_part(vc, 1, 1 - P);
       float mx = 0.f, ma;
       if constexpr (!(ABL & 4)) { if constexpr (P == 0) pl_y_0(va, mx, ma); else pl_y_1(va, mx, ma); }
       decide(mx);
@@ -1405,6 +1409,7 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 17: hipLaunchKernelGGL(attn_pl_kernel<6>, grid, dim3(256), 0, s, *a); break;
     case 18: hipLaunchKernelGGL(attn_pl_kernel<7>, grid, dim3(256), 0, s, *a); break;
     case 19: hipLaunchKernelGGL(attn_pl_kernel<32>, grid, dim3(256), 0, s, *a); break;
+    case 25: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<128>, grid, dim3(256), 0, s, *a); break;
     case 23: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<64>, grid, dim3(256), 0, s, *a); break;
     case 24: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<32>, grid, dim3(256), 0, s, *a); break;
     case 20: case 21: case 22: {  // asm pipeline at 8 waves x 32 queries (21: no tile loop, 22: no X / Y bodies)
