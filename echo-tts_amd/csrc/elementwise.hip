@@ -113,13 +113,26 @@ __global__ void __launch_bounds__(256) adaln_rows_kernel(const bf16_t* __restric
     load8(scale1 + (c * 64 + lane) * 8, s1[c]);
     load8(shift + (c * 64 + lane) * 8, sh[c]);
   }
+  // the next row's 16-B chunks are loaded before this row's sum / butterfly / stores (two rows in flight per wave)
+  uint4 raw[CH];
+  if (wave < rows) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) raw[c] = *(const uint4*)(x + (int64_t)wave * dim + (c * 64 + lane) * 8);
+  }
   for (int row = wave; row < rows; row += nwaves) {
-    const bf16_t* xr = x + (int64_t)row * dim;
     bf16_t* yr = y + (int64_t)row * dim;
     float v[CH][8];
     float ss = 0.f;
 #pragma unroll
-    for (int c = 0; c < CH; ++c) load8(xr + (c * 64 + lane) * 8, v[c]);
+    for (int c = 0; c < CH; ++c) {
+      const uint32_t w4[4] = {raw[c].x, raw[c].y, raw[c].z, raw[c].w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { v[c][2 * i] = bf2f(w4[i] & 0xffffu); v[c][2 * i + 1] = bf2f(w4[i] >> 16); }
+    }
+    if (row + nwaves < rows) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) raw[c] = *(const uint4*)(x + (int64_t)(row + nwaves) * dim + (c * 64 + lane) * 8);
+    }
 #pragma unroll
     for (int c = 0; c < CH; ++c)
 #pragma unroll
@@ -291,6 +304,9 @@ inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / p
     else return ECHO_EDTYPE;                                   \
   } while (0)
 
+// echo_gemm_set_diag key 9 (A/B timing only): block cap of the wave-per-row AdaLN kernel (0 = 8192)
+int g_adaln_blocks = 0;
+
 extern "C" {
 
 int echo_rmsnorm(int32_t dtype, const void* x, int64_t ldx, const void* w, void* y, int64_t ldy, int32_t rows,
@@ -308,8 +324,10 @@ int echo_adaln_modulate(int32_t dtype, const void* x, void* y, int32_t rows, int
   if (!x || !y || !shift || !scale1 || rows <= 0 || dim % 8 || dim > 8 * NB * 4) return ECHO_ESHAPE;
   if (rows_per_vec <= 0) rows_per_vec = rows;
   if (dtype == ECHO_BF16 && rows_per_vec >= rows && (dim == 1024 || dim == 2048 || dim == 4096)) {
-    // one vector pair for all rows: wave-per-row kernel, <= 8 rows per wave
-    const int blocks = min((rows + 3) / 4, 2048);
+    // one vector pair for all rows: wave-per-row kernel
+    // one row per wave up to 32768 rows (M = 30720: 39.2 vs 42.7 us with a 2048-block cap, the copy rate;
+    // tools/bench_adaln.py, profiles/r3_adaln_bw.txt); beyond that each wave prefetches its next row
+    const int blocks = min((rows + 3) / 4, g_adaln_blocks > 0 ? g_adaln_blocks : 8192);
     const hipStream_t st = (hipStream_t)stream;
     const bf16_t *xb = (const bf16_t*)x, *shb = (const bf16_t*)shift, *s1b = (const bf16_t*)scale1;
     bf16_t* yb = (bf16_t*)y;

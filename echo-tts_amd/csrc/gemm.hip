@@ -2026,6 +2026,8 @@ int g_gemm_no_colsplit = 0;  // key 8: no column split of 320-row launches (t320
 
 }  // namespace
 
+extern int g_adaln_blocks;  // elementwise.hip
+
 extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   if (value < 0) return ECHO_EINVAL;
   if (key == 1) g_gemm_stagger = value;
@@ -2036,6 +2038,7 @@ extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   else if (key == 6) g_gemm_ps_grid = value;
   else if (key == 7) { if (value > 2) return ECHO_EINVAL; g_gemm_t320 = value; }
   else if (key == 8) g_gemm_no_colsplit = value != 0;
+  else if (key == 9) g_adaln_blocks = value;
   else return ECHO_EINVAL;
   return 0;
 }

@@ -696,10 +696,11 @@ def test_attention_deferred_max_spikes():
     close_bf16(out, ref)
 
 
-@pytest.mark.parametrize("dim,rows", [(2048, 1), (2048, 9001), (1024, 37), (4096, 300)])
+@pytest.mark.parametrize("dim,rows", [(2048, 1), (2048, 9001), (2048, 30720), (1024, 37), (4096, 300)])
 def test_adaln_modulate_wave_rows(dim, rows):
     """The decoder's AdaLN tail (bf16, one vector pair for all rows): wave-per-row kernel, strided
-    over more rows than waves; one bf16 rounding of (x*r)*s1 + shift as the reference."""
+    over more rows than waves (30720: 3-4 rows per wave, the next row prefetched); one bf16 rounding of
+    (x*r)*s1 + shift as the reference."""
     x = torch.randn(rows, dim, device=DEV).to(BF)
     sh = torch.randn(dim, device=DEV).to(BF)
     s1 = (1 + 0.1 * torch.randn(dim, device=DEV)).to(BF)
