@@ -23,6 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("-o", default=None)
+    ap.add_argument("--calls", type=int, default=3,
+                    help="sampler calls in the profiled run (tools/gpu_pmc3.sh: 1 warmup + 2 timed)")
     args = ap.parse_args()
     acc = defaultdict(lambda: defaultdict(float))
     cnt = defaultdict(lambda: defaultdict(int))
@@ -53,11 +55,15 @@ def main():
     agg = sum(r["launches"] * (r["read_bytes_per_launch"] + r["write_bytes_per_launch"]) for r in out.values()
               if "read_bytes_per_launch" in r and "write_bytes_per_launch" in r)
     fam = round(agg / tot) if tot else None
-    print(f"family: {tot} launches, {fam} bytes per launch (read + write)")
+    per_call = round(agg / args.calls) if tot else None
+    print(f"family: {tot} launches, {fam} bytes per launch (read + write), {per_call} bytes per sampler call")
     if args.o:
+        # bench.py divides hbm_bytes_per_call by its roofline leg's GEMM call count: a column-split GEMM
+        # (two kernel launches) is one call there, as its algorithmic bytes are
         with open(args.o, "w") as f:
             json.dump({"source": args.root, "corrections": "FETCH_SIZE*1024*2, WRITE_SIZE*1024",
-                       "hbm_bytes_per_launch": fam, "kernels": out}, f, indent=1)
+                       "hbm_bytes_per_launch": fam, "hbm_bytes_per_call": per_call, "calls": args.calls,
+                       "kernels": out}, f, indent=1)
 
 
 if __name__ == "__main__":
