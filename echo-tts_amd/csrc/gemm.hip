@@ -1237,44 +1237,94 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
 // cW1 of tile k+1 in phase 0 of tile k: gemm_bf16_pp2_kernel's schedule and barrier argument with
 // c0-c2 -> cA + cW0 and c3 -> cW1, so the steady-state waits are vmcnt(9) (2 + 7 younger pieces).
 // Epilogue from registers, row fragment by row fragment (the residual rows of the next one in flight).
-template <int EK, int SP = 1>
-__global__ void __launch_bounds__(512)
-gemm_bf16_t320_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw,
-                      void* __restrict__ Cv, int64_t ldc, int M, int N, int K, int tiles_m, int tiles_n, Epi ep) {
+//
+// PER = 1 (persistent; production for SwiGLU, see launch_t320): one workgroup per CU walks tiles blockIdx.x, + gridDim.x, ... (gridDim.x a
+// multiple of 8, so t & 7 stays the XCD of the block-id map); after a tile's K loop the next tile's prologue
+// DMA is issued BEFORE its epilogue, so the first K-tile loads of tile i+1 are in flight under the epilogue
+// math and store burst of tile i (gemm_bf16_ps_kernel's scheme). vmcnt counts loads, LDS-DMA and stores in
+// issue order: the T320_SN(EK) stores of a wave are younger than the prologue DMA, so the prologue wait and
+// both waits of K-tile 0 allow T320_SN more in flight; K-tile 1's first wait (cW1 of tile 1, issued after
+// the stores) retires them. Same K loop, same per-element K order: bitwise equal to PER = 0.
+constexpr int t320_sn(int ek) { return ek == EK_SWIGLU ? 10 : 20; }  // stores per wave per tile (FM x 2 / FM x 4)
+
+// The epilogue reads its arguments (C, M, N, the Epi fields) through an opaque copy of the kernarg pointer taken
+// after each tile's K loop: otherwise hipcc hoists them out of the tile loop and holds them in SGPRs across the
+// K loop (106 SGPRs, spills into VGPRs at the 256-VGPR limit).
+struct T320Args {
+  const bf16_t* A; int64_t lda; const bf16_t* W; int64_t ldw;
+  void* Cv; int64_t ldc;
+  int M, N, K, tiles_m, tiles_n;
+  Epi ep;
+};
+
+template <int EK, int SP = 1, int PER = 0>
+__global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
   static_assert(EK == EK_RESID || EK == EK_SWIGLU || EK == EK_HEADNORM, "320-row tiles: residual / SwiGLU / head norm");
+  static_assert(!(PER && SP), "persistent form: 2 / 7 DMA split only");
+  using KA = const __attribute__((address_space(4))) T320Args;
+  KA* const kp0 = (KA*)__builtin_amdgcn_kernarg_segment_ptr();
+  (void)args;
+  // PER: the kernarg pointer through an opaque copy, so that values derived from the arguments at a tile
+  // boundary (origin, next-tile bases, epilogue arguments) are recomputed there instead of held across the loop
+  auto kargs = [&]() __attribute__((always_inline)) -> KA* {
+    uint64_t v = (uint64_t)kp0;
+    if constexpr (PER) asm volatile("" : "+s"(v));
+    return (KA*)v;
+  };
+  const int64_t lda = kp0->lda, ldw = kp0->ldw;
+  const int K = kp0->K;
   constexpr int BM = 320, BN = 256, TM = 80, TN = 128, FM = 5, FN = 8;
   constexpr int STAGE = (BM + BN) * BK;
+  constexpr int SN = t320_sn(EK);
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int grp = wid >> 2;  // ping-pong group: waves 4-7 run one barrier behind
-  const int nwg = tiles_m * tiles_n;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   constexpr int GM = 8;
-  const int gq = wg / (GM * tiles_n);
-  const int fm = gq * GM;
-  const int gm = min(tiles_m - fm, GM);
-  const int rem = wg - gq * GM * tiles_n;
-  const int m0 = (fm + rem % gm) * BM, n0 = (rem / gm) * BN;
+  // tile t -> origin: XCD-chunked (t & 7 = XCD) group-M order
+  auto origin = [&](int t, int& m0o, int& n0o) __attribute__((always_inline)) {
+    KA* const kq = kargs();
+    const int tiles_m = kq->tiles_m, tiles_n = kq->tiles_n;
+    const int nwg = tiles_m * tiles_n;
+    const int q8 = nwg >> 3, r8 = nwg & 7;
+    const int xcd = t & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (t >> 3);
+    const int gq = wg / (GM * tiles_n);
+    const int fm = gq * GM;
+    const int gm = min(tiles_m - fm, GM);
+    const int rem = wg - gq * GM * tiles_n;
+    m0o = (fm + rem % gm) * BM;
+    n0o = (rem / gm) * BN;
+  };
+  const int nwg = kp0->tiles_m * kp0->tiles_n;
+  int tcur = blockIdx.x;
+  if (PER && tcur >= nwg) return;
+  int m0, n0;
+  origin(tcur, m0, n0);
 
   // per-lane source offsets of an 8-row group (row rb + lane/8, chunk (lane&7) ^ ((row>>1)&7)); the
   // swizzle term depends only on the group's parity (rb/8 odd adds 4)
-  const int l8 = lane >> 3;
+  // (PER: recomputed from an opaque copy of the lane id at the top of every tile, so that they are dead
+  // during the epilogue, which runs at the 256-VGPR limit)
   uint32_t vA[2], vW[2];
+  auto lane_offsets = [&]() __attribute__((always_inline)) {
+    int ln = lane;
+    if constexpr (PER) asm volatile("" : "+v"(ln));
+    const int l8 = ln >> 3;
 #pragma unroll
-  for (int par = 0; par < 2; ++par) {
-    const int gc = (lane & 7) ^ ((4 * par + (l8 >> 1)) & 7);
-    vA[par] = (uint32_t)((l8 * lda + gc * 8) * 2);
-    vW[par] = (uint32_t)((l8 * ldw + gc * 8) * 2);
-  }
+    for (int par = 0; par < 2; ++par) {
+      const int gc = (ln & 7) ^ ((4 * par + (l8 >> 1)) & 7);
+      vA[par] = (uint32_t)((l8 * lda + gc * 8) * 2);
+      vW[par] = (uint32_t)((l8 * ldw + gc * 8) * 2);
+    }
+  };
+  lane_offsets();
   const uint32_t lds0 = lds_addr_of(lds);
-  const bf16_t* Ab = A + (int64_t)m0 * lda;
-  const bf16_t* Wb = W + (int64_t)n0 * ldw;
-  // chunk c (0 = cA, 1 = cW0, 2 = cW1) of K-tile kt into stage kt & 1
+  const bf16_t* Ab = kp0->A + (int64_t)m0 * lda;
+  const bf16_t* Wb = kp0->W + (int64_t)n0 * ldw;
+  // chunk c (0 = cA, 1 = cW0, 2 = cW1) of K-tile kt into stage kt & 1 (of the tile Ab / Wb point at)
   auto dma = [&](int c, int kt) __attribute__((always_inline)) {
     const uint32_t st = lds0 + (uint32_t)((kt & 1) * STAGE * 2);
     if (c == 0) {
@@ -1300,243 +1350,291 @@ gemm_bf16_t320_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* _
   // instead of two. Waits: phase 0 retires cW1(k) -> vmcnt(9) (cA(k+1) 5 + this phase's 4 younger), phase 1
   // retires cA(k+1) + cW0(k+1) -> vmcnt(7). Measured within +-1 % of the 2 / 7 schedule on every decoder
   // shape (profiles/r3_gemm_t320_dma_balance.txt): SP = 0 stays the default.
-  // prologue: tile 0 (cA, cW0, then cW1) and cA (SP) or cA + cW0 (!SP) of tile 1; wait for tile 0's cA + cW0
-  dma(0, 0); dma(1, 0); dma(2, 0);
-  if (nk > 1) {
-    dma(0, 1);
-    if constexpr (SP) { vm_wait_n<7>(); } else { dma(1, 1); vm_wait_n<9>(); }
-  } else {
-    vm_wait_n<2>();
-  }
-  pp_barrier();
-  if (grp == 1) pp_barrier();
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int frow = lane & 15;
-  const int fsw = frow >> 1;
-  bf16x8 af[FM][2], bfr[4][2];
-  for (int kt = 0; kt < nk; ++kt) {
-    const bf16_t* As = lds + (kt & 1) * STAGE;
-    const bf16_t* Bs = As + BM * BK;
-    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
-#pragma unroll
-    for (int ph = 0; ph < 2; ++ph) {
-      // ---- L segment
-      if (ph == 0) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int s = 0; s < 2; ++s)
-            af[i][s] = *(const bf16x8*)(As + (wm * TM + i * 16 + frow) * BK + (((4 * s + (lane >> 4)) ^ fsw) * 8));
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-          bfr[j][s] = *(const bf16x8*)(Bs + (wn * TN + ph * 64 + j * 16 + frow) * BK +
-                                       (((4 * s + (lane >> 4)) ^ fsw) * 8));
-      if constexpr (SP) {
-        if (ph == 0) {
-          if (n1) { dma(1, kt + 1); dma(2, kt + 1); }
-          // retire cW1 of tile kt (issued in phase 0 of tile kt-1 / the prologue)
-          if (n1) vm_wait_n<9>(); else vm_wait_n<0>();
-        } else {
-          if (n2) dma(0, kt + 2);
-          // retire cA + cW0 of tile kt+1
-          if (n2) vm_wait_n<7>(); else if (n1) vm_wait_n<2>(); else vm_wait_n<0>();
-        }
-      } else {
-        if (ph == 0) {
-          if (n1) dma(2, kt + 1);
-          // retire cW1 of tile kt (issued in phase 0 of tile kt-1 / the prologue)
-          if (n1) vm_wait_n<9>(); else vm_wait_n<0>();
-        } else {
-          if (n2) { dma(0, kt + 2); dma(1, kt + 2); }
-          // retire cA + cW0 of tile kt+1
-          if (n2) vm_wait_n<9>(); else if (n1) vm_wait_n<2>(); else vm_wait_n<0>();
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      pp_barrier();
-      // ---- C segment
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int s = 0; s < 2; ++s)
-            acc[i][ph * 4 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][s], af[i][s], acc[i][ph * 4 + j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      pp_barrier();
+  // prologue: tile 0 (cA, cW0, then cW1) and cA (SP) or cA + cW0 (!SP) of tile 1; the tile loop's first wait
+  // retires tile 0's cA + cW0 (PER: the previous tile's SN stores are younger and stay in flight)
+  auto prologue = [&]() __attribute__((always_inline)) {
+    dma(0, 0); dma(1, 0); dma(2, 0);
+    if (nk > 1) {
+      dma(0, 1);
+      if constexpr (!SP) dma(1, 1);
     }
-  }
-  if (grp == 0) pp_barrier();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  prologue();
 
   // ---- epilogue: out = bf16(x + bf16(g * bf16(acc))) (the persistent kernel's RESID kind). A lane holds
   // rows mb + 16 ii, columns 16 j + 4 (lane >> 4) .. + 3 of the wave's 128; one v_permlane16_swap per
   // packed word of a fragment pair (2p, 2p+1) gives it 8 consecutive columns (16-B accesses).
-  const int g4 = lane >> 4;
-  const int cpos = (g4 & 1) * 16 + (g4 >> 1) * 8;
-  const int mb = m0 + wm * TM + (lane & 15);
-  const int nb = n0 + wn * TN + cpos;
-  const __amdgpu_buffer_rsrc_t crs =
-      brsrc(Cv, (uint32_t)(((int64_t)(M - 1) * ldc + (EK == EK_SWIGLU ? N / 2 : N)) * 2));
   auto swap_pair = [&](uint2 lo, uint2 hi) __attribute__((always_inline)) -> u32x4 {
     const auto s0 = __builtin_amdgcn_permlane16_swap(lo.x, hi.x, false, false);
     const auto s1 = __builtin_amdgcn_permlane16_swap(lo.y, hi.y, false, false);
     return u32x4{s0[0], s1[0], s0[1], s1[1]};
   };
-  if constexpr (EK == EK_HEADNORM) {
-    // q/k RMSNorm + half RoPE (ECHO_EPI_HEADNORM), bitwise equal to the persistent kernel's HEADNORM kind
-    // and to echo_head_norm_rope: v = bf16(acc); per 8-column chunk c of the head the sum of squares in
-    // column order from 0; then the butterfly's tree over chunks (c ^ 8, c ^ 4, c ^ 2, c ^ 1); r = 1 /
-    // sqrtf(ss / 128 + eps); v = bf16(v * r * w); RoPE on column pairs in fp32; one rounding at the store.
-    // Here a wave's 128 columns are one whole head: chunk 2j + (g >> 1) of column fragment j (g = lane >> 4),
-    // its columns 0-3 in lanes g = 0, 2 and 4-7 in g = 1, 3 (one lane ^ 16 exchange); c ^ 8 is fragment
-    // j ^ 4 and c ^ 4, c ^ 2 fragments j ^ 2, j ^ 1 of the same lane; c ^ 1 is lane ^ 32.
-    const int hidx = (n0 + wn * TN) >> 7;
-    const int hblk = hidx / ep.hn_heads, hhd = hidx - hblk * ep.hn_heads;
-    const bool hnorm = hblk < ep.hn_nblk, hrope = hnorm && hhd < ep.hn_rope_heads;
-    const bool hi16 = (g4 & 1) != 0;
-    auto unpack = [](uint2 u, float (&v)[4]) __attribute__((always_inline)) {
-      v[0] = bf2f(u.x & 0xffffu); v[1] = bf2f(u.x >> 16); v[2] = bf2f(u.y & 0xffffu); v[3] = bf2f(u.y >> 16);
-    };
-    uint2 hw[FN];
-    if (hnorm) {
-      const bf16_t* wp = (const bf16_t*)ep.hn_w + hblk * ep.hn_w_stride + hhd * 128 + 4 * g4;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) hw[j] = *(const uint2*)(wp + j * 16);
+  bool first = true;
+  for (;;) {
+    if (PER && !first) lane_offsets();
+    if (nk > 1) {
+      if constexpr (SP) vm_wait_n<7>();
+      else if (first) vm_wait_n<9>();
+      else vm_wait_n<9 + SN>();
+    } else {
+      if (first) vm_wait_n<2>(); else vm_wait_n<2 + SN>();
     }
+    pp_barrier();
+    if (grp == 1) pp_barrier();
+
+    // fragment-read lane terms (PER: from an opaque lane copy per tile, dead during the epilogue)
+    int lf = lane;
+    if constexpr (PER) asm volatile("" : "+v"(lf));
+    const int frow = lf & 15, fq = lf >> 4;
+    const int fsw = frow >> 1;
+    f32x4 acc[FM][FN];
 #pragma unroll
-    for (int ii = 0; ii < FM; ++ii) {
-      const int m = mb + ii * 16;
-      float4 rc[FN];
-      if (hrope) {  // (cos, sin) of the lane's 2 column pairs per fragment, in flight during the sums
-        const int pos = ep.hn_pos0 + ep.hn_pos_mult * (min(m, M - 1) % ep.hn_seq_len);
-        const float* rp = ep.hn_rope + ((int64_t)pos * 64 + 2 * g4) * 2;
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) rc[j] = *(const float4*)(rp + j * 16);
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 af[FM][2], bfr[4][2];
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16_t* As = lds + (kt & 1) * STAGE;
+      const bf16_t* Bs = As + BM * BK;
+      const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+      const bool xs = PER && !first && kt == 0;  // the previous tile's SN stores are still counted
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph) {
+        // ---- L segment
+        if (ph == 0) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              af[i][s] = *(const bf16x8*)(As + (wm * TM + i * 16 + frow) * BK + (((4 * s + fq) ^ fsw) * 8));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            bfr[j][s] = *(const bf16x8*)(Bs + (wn * TN + ph * 64 + j * 16 + frow) * BK + (((4 * s + fq) ^ fsw) * 8));
+        if constexpr (SP) {
+          if (ph == 0) {
+            if (n1) { dma(1, kt + 1); dma(2, kt + 1); }
+            // retire cW1 of tile kt (issued in phase 0 of tile kt-1 / the prologue)
+            if (n1) vm_wait_n<9>(); else vm_wait_n<0>();
+          } else {
+            if (n2) dma(0, kt + 2);
+            // retire cA + cW0 of tile kt+1
+            if (n2) vm_wait_n<7>(); else if (n1) vm_wait_n<2>(); else vm_wait_n<0>();
+          }
+        } else {
+          if (ph == 0) {
+            if (n1) dma(2, kt + 1);
+            // retire cW1 of tile kt (issued in phase 0 of tile kt-1 / the prologue)
+            if (n1) { if (xs) vm_wait_n<9 + SN>(); else vm_wait_n<9>(); } else vm_wait_n<0>();
+          } else {
+            if (n2) { dma(0, kt + 2); dma(1, kt + 2); }
+            // retire cA + cW0 of tile kt+1
+            if (n2) { if (xs) vm_wait_n<9 + SN>(); else vm_wait_n<9>(); }
+            else if (n1) { if (xs) vm_wait_n<2 + SN>(); else vm_wait_n<2>(); }
+            else vm_wait_n<0>();
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pp_barrier();
+        // ---- C segment
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              acc[i][ph * 4 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][s], af[i][s], acc[i][ph * 4 + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        pp_barrier();
       }
-      uint2 hp[FN];
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        hp[j] = make_uint2(pack2bf(acc[ii][j][0], acc[ii][j][1]), pack2bf(acc[ii][j][2], acc[ii][j][3]));
+    }
+    if (grp == 0) pp_barrier();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    bool more = false;
+    int m0n = 0, n0n = 0;
+    if constexpr (PER) {
+      // every wave's last fragment reads are retired: both LDS stages take the next tile's prologue DMA
+      pp_barrier();
+      tcur += gridDim.x;
+      more = tcur < nwg;
+      if (more) {
+        origin(tcur, m0n, n0n);
+        KA* const kq = kargs();
+        Ab = kq->A + (int64_t)m0n * lda;
+        Wb = kq->W + (int64_t)n0n * ldw;
+        lane_offsets();
+        prologue();
+      }
+    }
+    KA* const kp = kargs();
+    auto& ep = kp->ep;
+    const int M = kp->M, N = kp->N;
+    const int64_t ldc = kp->ldc;
+    const __amdgpu_buffer_rsrc_t crs =
+        brsrc(kp->Cv, (uint32_t)(((int64_t)(M - 1) * ldc + (EK == EK_SWIGLU ? N / 2 : N)) * 2));
+    // lane-derived epilogue values from an opaque copy of the lane id (PER: not hoisted out of the tile loop,
+    // where they would stay live across the K loop)
+    int le = lane;
+    if constexpr (PER) asm volatile("" : "+v"(le));
+    const int g4 = le >> 4;
+    const int cpos = (g4 & 1) * 16 + (g4 >> 1) * 8;
+    const int mb = m0 + wm * TM + (le & 15);
+    const int nb = n0 + wn * TN + cpos;
+
+    if constexpr (EK == EK_HEADNORM) {
+      // q/k RMSNorm + half RoPE (ECHO_EPI_HEADNORM), bitwise equal to the persistent kernel's HEADNORM kind
+      // and to echo_head_norm_rope: v = bf16(acc); per 8-column chunk c of the head the sum of squares in
+      // column order from 0; then the butterfly's tree over chunks (c ^ 8, c ^ 4, c ^ 2, c ^ 1); r = 1 /
+      // sqrtf(ss / 128 + eps); v = bf16(v * r * w); RoPE on column pairs in fp32; one rounding at the store.
+      // Here a wave's 128 columns are one whole head: chunk 2j + (g >> 1) of column fragment j (g = lane >> 4),
+      // its columns 0-3 in lanes g = 0, 2 and 4-7 in g = 1, 3 (one lane ^ 16 exchange); c ^ 8 is fragment
+      // j ^ 4 and c ^ 4, c ^ 2 fragments j ^ 2, j ^ 1 of the same lane; c ^ 1 is lane ^ 32.
+      const int hidx = (n0 + wn * TN) >> 7;
+      const int hblk = hidx / ep.hn_heads, hhd = hidx - hblk * ep.hn_heads;
+      const bool hnorm = hblk < ep.hn_nblk, hrope = hnorm && hhd < ep.hn_rope_heads;
+      const bool hi16 = (g4 & 1) != 0;
+      auto unpack = [](uint2 u, float (&v)[4]) __attribute__((always_inline)) {
+        v[0] = bf2f(u.x & 0xffffu); v[1] = bf2f(u.x >> 16); v[2] = bf2f(u.y & 0xffffu); v[3] = bf2f(u.y >> 16);
+      };
+      uint2 hw[FN];
       if (hnorm) {
-        float c8[FN];
+        const bf16_t* wp = (const bf16_t*)ep.hn_w + hblk * ep.hn_w_stride + hhd * 128 + 4 * g4;
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          float v[4];
-          unpack(hp[j], v);
-          float h = 0.f;
+        for (int j = 0; j < FN; ++j) hw[j] = *(const uint2*)(wp + j * 16);
+      }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) h += v[e] * v[e];   // columns 0-3 (lanes g = 0, 2)
-          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(h), __float_as_uint(h), false, false);
-          float c = __uint_as_float(hi16 ? sw[0] : sw[1]);  // lane ^ 16's partial
+      for (int ii = 0; ii < FM; ++ii) {
+        const int m = mb + ii * 16;
+        float4 rc[FN];
+        if (hrope) {  // (cos, sin) of the lane's 2 column pairs per fragment, in flight during the sums
+          const int pos = ep.hn_pos0 + ep.hn_pos_mult * (min(m, M - 1) % ep.hn_seq_len);
+          const float* rp = ep.hn_rope + ((int64_t)pos * 64 + 2 * g4) * 2;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) c += v[e] * v[e];  // columns 4-7: the chunk's sum (lanes g = 1, 3)
-          c8[j] = c;
+          for (int j = 0; j < FN; ++j) rc[j] = *(const float4*)(rp + j * 16);
         }
-        const float t3 = ((c8[0] + c8[4]) + (c8[2] + c8[6])) + ((c8[1] + c8[5]) + (c8[3] + c8[7]));
-        const auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(t3), __float_as_uint(t3), false, false);
-        const float t4 = t3 + __uint_as_float(lane >= 32 ? s32[0] : s32[1]);   // c ^ 1 (lane ^ 32)
-        const float r = 1.0f / sqrtf(t4 / 128.0f + ep.hn_eps);
-        const auto sr = __builtin_amdgcn_permlane16_swap(__float_as_uint(r), __float_as_uint(r), false, false);
-        const float rr = hi16 ? r : __uint_as_float(sr[1]);  // lanes g = 0, 2 take lane ^ 16's
+        uint2 hp[FN];
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          float v[4], wv[4];
-          unpack(hp[j], v);
-          unpack(hw[j], wv);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = (v[e] * rr) * wv[e];
-          hp[j] = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));   // bf16(v * r * w)
-        }
-        if (hrope) {
+        for (int j = 0; j < FN; ++j)
+          hp[j] = make_uint2(pack2bf(acc[ii][j][0], acc[ii][j][1]), pack2bf(acc[ii][j][2], acc[ii][j][3]));
+        if (hnorm) {
+          float c8[FN];
 #pragma unroll
           for (int j = 0; j < FN; ++j) {
             float v[4];
             unpack(hp[j], v);
-            const float4 cs = rc[j];
-            const float y0 = (v[0] * cs.x) - (v[1] * cs.y), y1 = (v[0] * cs.y) + (v[1] * cs.x);
-            const float y2 = (v[2] * cs.z) - (v[3] * cs.w), y3 = (v[2] * cs.w) + (v[3] * cs.z);
-            hp[j] = make_uint2(pack2bf(y0, y1), pack2bf(y2, y3));
+            float h = 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) h += v[e] * v[e];   // columns 0-3 (lanes g = 0, 2)
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(h), __float_as_uint(h), false, false);
+            float c = __uint_as_float(hi16 ? sw[0] : sw[1]);  // lane ^ 16's partial
+#pragma unroll
+            for (int e = 0; e < 4; ++e) c += v[e] * v[e];  // columns 4-7: the chunk's sum (lanes g = 1, 3)
+            c8[j] = c;
+          }
+          const float t3 = ((c8[0] + c8[4]) + (c8[2] + c8[6])) + ((c8[1] + c8[5]) + (c8[3] + c8[7]));
+          const auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(t3), __float_as_uint(t3), false, false);
+          const float t4 = t3 + __uint_as_float(le >= 32 ? s32[0] : s32[1]);   // c ^ 1 (lane ^ 32)
+          const float r = 1.0f / sqrtf(t4 / 128.0f + ep.hn_eps);
+          const auto sr = __builtin_amdgcn_permlane16_swap(__float_as_uint(r), __float_as_uint(r), false, false);
+          const float rr = hi16 ? r : __uint_as_float(sr[1]);  // lanes g = 0, 2 take lane ^ 16's
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            float v[4], wv[4];
+            unpack(hp[j], v);
+            unpack(hw[j], wv);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = (v[e] * rr) * wv[e];
+            hp[j] = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));   // bf16(v * r * w)
+          }
+          if (hrope) {
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+              float v[4];
+              unpack(hp[j], v);
+              const float4 cs = rc[j];
+              const float y0 = (v[0] * cs.x) - (v[1] * cs.y), y1 = (v[0] * cs.y) + (v[1] * cs.x);
+              const float y2 = (v[2] * cs.z) - (v[3] * cs.w), y3 = (v[2] * cs.w) + (v[3] * cs.z);
+              hp[j] = make_uint2(pack2bf(y0, y1), pack2bf(y2, y3));
+            }
           }
         }
+        const uint32_t off = (uint32_t)((m * ldc + nb) * 2);
+#pragma unroll
+        for (int p = 0; p < FN / 2; ++p)
+          __builtin_amdgcn_raw_buffer_store_b128(swap_pair(hp[2 * p], hp[2 * p + 1]), crs, off + p * 64, 0, 0);
+        // PER: one row fragment at a time (hipcc otherwise hoists the next fragments' table loads and spills)
+        if constexpr (PER) __builtin_amdgcn_sched_barrier(0);
       }
-      const uint32_t off = (uint32_t)((m * ldc + nb) * 2);
+    } else if constexpr (EK == EK_SWIGLU) {
+      // gate / up column blocks interleaved by 16 (fragment 2jo gate, 2jo+1 up of output fragment jo): the
+      // persistent kernel's SwiGLU kind; output fragments (2p, 2p+1) form the swapped pair of 8 columns
+      const int nbo = n0 / 2 + wn * (TN / 2) + cpos;
 #pragma unroll
-      for (int p = 0; p < FN / 2; ++p)
-        __builtin_amdgcn_raw_buffer_store_b128(swap_pair(hp[2 * p], hp[2 * p + 1]), crs, off + p * 64, 0, 0);
-    }
-    return;
-  }
-  if constexpr (EK == EK_SWIGLU) {
-    // gate / up column blocks interleaved by 16 (fragment 2jo gate, 2jo+1 up of output fragment jo): the
-    // persistent kernel's SwiGLU kind; output fragments (2p, 2p+1) form the swapped pair of 8 columns
-    const int nbo = n0 / 2 + wn * (TN / 2) + cpos;
+      for (int ii = 0; ii < FM; ++ii) {
 #pragma unroll
-    for (int ii = 0; ii < FM; ++ii) {
+        for (int p = 0; p < 2; ++p) {
+          uint2 q[2];
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        uint2 q[2];
+          for (int jj = 0; jj < 2; ++jj) {
+            float u[4];
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          float u[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float a = rbf(acc[ii][4 * p + 2 * jj][r]), b = rbf(acc[ii][4 * p + 2 * jj + 1][r]);
-            u[r] = rbf(silu_bf16in(a)) * b;
+            for (int r = 0; r < 4; ++r) {
+              const float a = rbf(acc[ii][4 * p + 2 * jj][r]), b = rbf(acc[ii][4 * p + 2 * jj + 1][r]);
+              u[r] = rbf(silu_bf16in(a)) * b;
+            }
+            q[jj] = make_uint2(pack2bf(u[0], u[1]), pack2bf(u[2], u[3]));
           }
-          q[jj] = make_uint2(pack2bf(u[0], u[1]), pack2bf(u[2], u[3]));
+          __builtin_amdgcn_raw_buffer_store_b128(swap_pair(q[0], q[1]), crs,
+                                                 (uint32_t)(((mb + ii * 16) * ldc + nbo + p * 32) * 2), 0, 0);
         }
-        __builtin_amdgcn_raw_buffer_store_b128(swap_pair(q[0], q[1]), crs,
-                                               (uint32_t)(((mb + ii * 16) * ldc + nbo + p * 32) * 2), 0, 0);
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t ars = brsrc(ep.aux, (uint32_t)(((int64_t)(M - 1) * ep.ld_aux + N) * 2));
+      u32x4 gv[FN / 2];
+      if (ep.gate) {
+#pragma unroll
+        for (int p = 0; p < FN / 2; ++p) gv[p] = *(const u32x4*)((const bf16_t*)ep.gate + nb + p * 32);
+      }
+      u32x4 xr[2][FN / 2];
+      auto load_x = [&](int ii, u32x4 (&d)[FN / 2]) __attribute__((always_inline)) {
+        const uint32_t off = (uint32_t)(((mb + ii * 16) * ep.ld_aux + nb) * 2);
+#pragma unroll
+        for (int p = 0; p < FN / 2; ++p)
+          d[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ars, off + p * 64, 0, 0));
+      };
+      load_x(0, xr[0]);
+#pragma unroll
+      for (int ii = 0; ii < FM; ++ii) {
+        if (ii + 1 < FM) load_x(ii + 1, xr[(ii + 1) & 1]);
+        const uint32_t off = (uint32_t)(((mb + ii * 16) * ldc + nb) * 2);
+#pragma unroll
+        for (int p = 0; p < FN / 2; ++p) {
+          const f32x4 c0 = acc[ii][2 * p], c1 = acc[ii][2 * p + 1];
+          u32x4 o = swap_pair(make_uint2(pack2bf(c0[0], c0[1]), pack2bf(c0[2], c0[3])),
+                              make_uint2(pack2bf(c1[0], c1[1]), pack2bf(c1[2], c1[3])));
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            float v0 = bf2f(o[w] & 0xffffu), v1 = bf2f(o[w] >> 16);
+            if (ep.gate) {
+              v0 = rbf(bf2f(gv[p][w] & 0xffffu) * v0);
+              v1 = rbf(bf2f(gv[p][w] >> 16) * v1);
+            }
+            v0 = bf2f(xr[ii & 1][p][w] & 0xffffu) + v0;
+            v1 = bf2f(xr[ii & 1][p][w] >> 16) + v1;
+            o[w] = pack2bf(v0, v1);
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(o, crs, off + p * 64, 0, 0);
+        }
       }
     }
-    return;
-  }
-  const __amdgpu_buffer_rsrc_t ars = brsrc(ep.aux, (uint32_t)(((int64_t)(M - 1) * ep.ld_aux + N) * 2));
-  u32x4 gv[FN / 2];
-  if (ep.gate) {
-#pragma unroll
-    for (int p = 0; p < FN / 2; ++p) gv[p] = *(const u32x4*)((const bf16_t*)ep.gate + nb + p * 32);
-  }
-  u32x4 xr[2][FN / 2];
-  auto load_x = [&](int ii, u32x4 (&d)[FN / 2]) __attribute__((always_inline)) {
-    const uint32_t off = (uint32_t)(((mb + ii * 16) * ep.ld_aux + nb) * 2);
-#pragma unroll
-    for (int p = 0; p < FN / 2; ++p)
-      d[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ars, off + p * 64, 0, 0));
-  };
-  load_x(0, xr[0]);
-#pragma unroll
-  for (int ii = 0; ii < FM; ++ii) {
-    if (ii + 1 < FM) load_x(ii + 1, xr[(ii + 1) & 1]);
-    const uint32_t off = (uint32_t)(((mb + ii * 16) * ldc + nb) * 2);
-#pragma unroll
-    for (int p = 0; p < FN / 2; ++p) {
-      const f32x4 c0 = acc[ii][2 * p], c1 = acc[ii][2 * p + 1];
-      u32x4 o = swap_pair(make_uint2(pack2bf(c0[0], c0[1]), pack2bf(c0[2], c0[3])),
-                          make_uint2(pack2bf(c1[0], c1[1]), pack2bf(c1[2], c1[3])));
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        float v0 = bf2f(o[w] & 0xffffu), v1 = bf2f(o[w] >> 16);
-        if (ep.gate) {
-          v0 = rbf(bf2f(gv[p][w] & 0xffffu) * v0);
-          v1 = rbf(bf2f(gv[p][w] >> 16) * v1);
-        }
-        v0 = bf2f(xr[ii & 1][p][w] & 0xffffu) + v0;
-        v1 = bf2f(xr[ii & 1][p][w] >> 16) + v1;
-        o[w] = pack2bf(v0, v1);
-      }
-      __builtin_amdgcn_raw_buffer_store_b128(o, crs, off + p * 64, 0, 0);
-    }
+    if (!more) break;
+    m0 = m0n;
+    n0 = n0n;
+    first = false;
   }
 }
 
@@ -1967,22 +2065,34 @@ bool t320_ok(const EchoGemmArgs* a) {
   return true;
 }
 
-template <int SP>
+int g_gemm_t320_np = 0;  // echo_gemm_set_diag key 10: 1 = the non-persistent 320-row kernel (A/B)
+
+// PER = 1: one persistent workgroup per CU (grid = min(tiles, CUs rounded down to a multiple of 8))
+template <int SP, int PER>
 int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   const int tm = a->M / 320, tn = a->N / 256;
+  int grid = tm * tn;
+  if (PER) {
+    const int cus = cu_count_cached() & ~7;
+    if (cus >= 8 && grid > cus) grid = cus;
+  }
+  const T320Args ta{(const bf16_t*)a->A, a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep};
   if (ek_of(a) == EK_SWIGLU)
-    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_SWIGLU, SP>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A,
-                       a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep);
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_SWIGLU, SP, PER>), dim3(grid), dim3(512), 0, s, ta);
   else if (ek_of(a) == EK_HEADNORM)
-    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_HEADNORM, SP>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A,
-                       a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep);
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_HEADNORM, SP, PER>), dim3(grid), dim3(512), 0, s, ta);
   else
-    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_RESID, SP>), dim3(tm * tn), dim3(512), 0, s, (const bf16_t*)a->A,
-                       a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep);
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_RESID, SP, PER>), dim3(grid), dim3(512), 0, s, ta);
   ECHO_LAUNCH_CHECK();
   return 0;
 }
-int launch_t320(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) { return launch_t320_sp<0>(a, ep, s); }
+// production 320-row launch: the persistent form for SwiGLU (W13: 15 / 5 tiles per CU at M = 30720 / 10240,
+// -2.5 / -3 %, profiles/r3_t320_persistent.txt) unless diag key 10 asks for one tile per workgroup; one tile
+// per workgroup for the gated residual (3 / 1 tiles per CU, K = 5888 for W2: no measurable gain) and the
+// head-norm epilogue (whose register epilogue spills in the persistent form: +22 % at M = 30720)
+int launch_t320(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
+  return (ek_of(a) == EK_SWIGLU && !g_gemm_t320_np) ? launch_t320_sp<0, 1>(a, ep, s) : launch_t320_sp<0, 0>(a, ep, s);
+}
 
 // auto pick between 320x256 and 256x256 tiles by whole rounds of the CUs: a 320-row tile does 1.25x the work
 // of a 256-row one in ≈1.2x the time (more MFMA per staged byte; HEADNORM: one wave per head, no LDS
@@ -2039,6 +2149,7 @@ extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   else if (key == 7) { if (value > 2) return ECHO_EINVAL; g_gemm_t320 = value; }
   else if (key == 8) g_gemm_no_colsplit = value != 0;
   else if (key == 9) g_adaln_blocks = value;
+  else if (key == 10) g_gemm_t320_np = value != 0;
   else return ECHO_EINVAL;
   return 0;
 }
@@ -2085,7 +2196,7 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   // fused on the persistent kernel (t 16/17/18, N % 256 == 0, via ps_ok) or the 2-phase one (t 13)
   const bool hn_fused = a->dtype == ECHO_BF16 && ((t == 13 && a->N % 128 == 0) ||
                                                    ((t == 16 || t == 17 || t == 18) && ps_ok(a, EK_HEADNORM)) ||
-                                                   ((t == 20 || t == 21) && t320_ok(a)));
+                                                   ((t >= 20 && t <= 23) && t320_ok(a)));
   if (headnorm && !hn_fused) {
     // not fused for this shape / dtype: plain store, then the standalone kernel (same results)
     EchoGemmArgs b = *a;
@@ -2117,7 +2228,9 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
   // gated residual / SwiGLU / head norm at M = 320 k: 320-row tiles when they need fewer 1.2x tile-rounds than
   // 256x256 tiles (t320_pays); tile 20 forces them (bitwise equal either way)
   if (a->tile == 20) return t320_ok(a) ? launch_t320(a, ep, s) : ECHO_EINVAL;
-  if (a->tile == 21) return t320_ok(a) ? launch_t320_sp<1>(a, ep, s) : ECHO_EINVAL;  // 4 / 5 DMA split (A/B)
+  if (a->tile == 21) return t320_ok(a) ? launch_t320_sp<1, 0>(a, ep, s) : ECHO_EINVAL;  // 4 / 5 DMA split (A/B)
+  if (a->tile == 22) return t320_ok(a) ? launch_t320_sp<0, 0>(a, ep, s) : ECHO_EINVAL;  // one tile per workgroup
+  if (a->tile == 23) return t320_ok(a) ? launch_t320_sp<0, 1>(a, ep, s) : ECHO_EINVAL;  // persistent
   if (a->tile == 0 && g_gemm_t320 == 0 && !g_gemm_no_colsplit && a->batch == 1 && !headnorm && t320_ok(a)) {
     const int c1 = t320_col_split(a, cu_count_cached());
     if (c1 > 0) {

@@ -96,7 +96,9 @@ int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch);
  * key 7: 320x256 tiles for the gated residual / SwiGLU / head norm (0 = when they need fewer 1.2x
  * tile-rounds than 256x256 tiles, 1 = never, 2 = whenever they fill at least one round); key 8: 1 = no
  * column split of auto-picked 320-row launches (W13: 320-row tiles on whole rounds of tile columns, the
- * rest on the persistent 256x256 kernel); key 9: block cap of the wave-per-row AdaLN kernel (0 = 8192) (A/B timing, tools/bench_streams.py --diag; all bitwise-equal). */
+ * rest on the persistent 256x256 kernel); key 9: block cap of the wave-per-row AdaLN kernel (0 = 8192);
+ * key 10: 1 = one 320-row tile per workgroup instead of the persistent 320-row SwiGLU kernel (`tile` 22 / 23
+ * force either form for any epilogue) (A/B timing, tools/bench_streams.py --diag; all bitwise-equal). */
 int echo_gemm_set_diag(int32_t key, int32_t value);
 
 /* One key/value segment of the joint attention (model.py:246-253): rows of

@@ -180,7 +180,8 @@ def test_gemm_persistent_bias_bitwise(M, N, K):
 @pytest.mark.parametrize("M,N,K", [(30720, 2048, 2048), (10240, 2048, 5888), (10240, 11776, 128), (640, 512, 128),
                                    (960, 768, 192)])
 def test_gemm_t320_bitwise(M, N, K):
-    """320x256 tiles (tile 20; the auto pick for the N = 2048 gated residual when they fill whole rounds):
+    """320x256 tiles (tile 20 = the production persistent form, 23 forced persistent, 22 one tile per workgroup,
+    21 the balanced-DMA variant; the auto pick for the N = 2048 gated residual when they fill whole rounds):
     same per-element K order as the 256x256 kernels, so bitwise equal to the 2-phase kernel (tile 13) and to
     the auto pick (N = 11776: column split, 320-row tiles on the first 40 tile columns), with and without gate, in place on a column slice of a wider buffer (padding untouched);
     close to an fp32 reference."""
@@ -190,7 +191,7 @@ def test_gemm_t320_bitwise(M, N, K):
     h = torch.randn(M, N + 256, device=DEV).to(BF)
     for gate in (g, None):
         outs = []
-        for tile in (13, 20, 21, 0):
+        for tile in (13, 20, 21, 22, 23, 0):
             buf = h.clone()
             ops.gemm(a, w, out=buf[:, :N], epilogue=L.EPI_RESID, aux=buf[:, :N], gate=gate, tile=tile)
             assert torch.equal(buf[:, N:], h[:, N:])
@@ -208,12 +209,13 @@ def test_gemm_t320_bitwise(M, N, K):
 def test_gemm_t320_swiglu_bitwise(M, N, K):
     """320x256 tiles with the SwiGLU epilogue (W13 at M = 30720 / 10240: the auto pick splits the columns,
     320-row tiles on the first 40 tile columns, the persistent 256x256 kernel on the last 6): bitwise equal
-    to the 2-phase kernel and the auto pick; output a column slice of a wider buffer (padding untouched)."""
+    to the 2-phase kernel and the auto pick, persistent (tiles 20 / 23: 17.25 tiles per CU at M = 30720) or not
+    (22); output a column slice of a wider buffer (padding untouched)."""
     a = torch.randn(M, K, device=DEV).to(BF)
     w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
     h = torch.randn(M, N // 2 + 256, device=DEV).to(BF)
     outs = []
-    for tile in (13, 20, 21, 0):
+    for tile in (13, 20, 21, 22, 23, 0):
         buf = h.clone()
         ops.gemm(a, w, out=buf[:, :N // 2], epilogue=L.EPI_SWIGLU, tile=tile)
         assert torch.equal(buf[:, N // 2:], h[:, N // 2:])
@@ -795,7 +797,7 @@ def test_gemm_headnorm_t320(M, H, pos0, rh, K):
     ops.head_norm_rope(ref, H, nw, 1e-5, nblk=2, col0=0, col_stride=H * 128, w_stride=H * 128, rope=rope,
                        rope_heads=rh, seq_len=seq, pos0=pos0)
     hn = ops.HeadNorm(nw, H, 2, 1e-5, w_stride=H * 128, rope=rope, rope_heads=rh, seq_len=seq, pos0=pos0)
-    for tile in (20, 21, 0, 13):
+    for tile in (20, 21, 22, 23, 0, 13):
         got = ops.gemm(a, w, tile=tile, head_norm=hn)
         assert torch.equal(got, ref), tile
 

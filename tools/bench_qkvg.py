@@ -41,8 +41,14 @@ def main():
         def fused_pp2():
             ops.gemm(x, w, out=out, head_norm=hn, tile=13)
 
-        def fused_t320():  # 320x256 tiles (tile 20; rows must be a multiple of 320)
+        def fused_t320():  # 320x256 tiles (tile 20 = production form; rows must be a multiple of 320)
             ops.gemm(x, w, out=out, head_norm=hn, tile=20 if M % 320 == 0 else 0)
+
+        def fused_t320np():  # 320x256 tiles, one tile per workgroup (tile 22)
+            ops.gemm(x, w, out=out, head_norm=hn, tile=22 if M % 320 == 0 else 0)
+
+        def fused_t320p():  # 320x256 tiles, persistent (tile 23)
+            ops.gemm(x, w, out=out, head_norm=hn, tile=23 if M % 320 == 0 else 0)
 
         def fused_ps():  # the 256x256 persistent kernel (tile 16)
             ops.gemm(x, w, out=out, head_norm=hn, tile=16)
@@ -66,7 +72,11 @@ def main():
         same = same and bool(torch.equal(a, out))
         fused_t320()
         same = same and bool(torch.equal(a, out))
-        arms = (("fused", fused), ("fused_ps", fused_ps), ("fused_t320", fused_t320), ("fused_pp2", fused_pp2),
+        for fn in (fused_t320np, fused_t320p):
+            fn()
+            same = same and bool(torch.equal(a, out))
+        arms = (("fused", fused), ("fused_ps", fused_ps), ("fused_t320", fused_t320), ("fused_t320np", fused_t320np),
+                ("fused_t320p", fused_t320p), ("fused_pp2", fused_pp2),
                 ("split", split), ("store_ps", store_ps), ("store_pp2", store_pp2))
         times = {k: [] for k, _ in arms}
         for _ in range(args.rounds):
