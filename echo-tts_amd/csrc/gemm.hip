@@ -1500,6 +1500,14 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
       auto unpack = [](uint2 u, float (&v)[4]) __attribute__((always_inline)) {
         v[0] = bf2f(u.x & 0xffffu); v[1] = bf2f(u.x >> 16); v[2] = bf2f(u.y & 0xffffu); v[3] = bf2f(u.y >> 16);
       };
+      // the store rounding first for the whole tile: bf16(acc), 2 per register (80 VGPRs instead of the 160 of
+      // acc, which is dead after this: room for the table loads without spills)
+      uint2 hpa[FM][FN];
+#pragma unroll
+      for (int ii = 0; ii < FM; ++ii)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          hpa[ii][j] = make_uint2(pack2bf(acc[ii][j][0], acc[ii][j][1]), pack2bf(acc[ii][j][2], acc[ii][j][3]));
       uint2 hw[FN];
       if (hnorm) {
         const bf16_t* wp = (const bf16_t*)ep.hn_w + hblk * ep.hn_w_stride + hhd * 128 + 4 * g4;
@@ -1518,8 +1526,7 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
         }
         uint2 hp[FN];
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          hp[j] = make_uint2(pack2bf(acc[ii][j][0], acc[ii][j][1]), pack2bf(acc[ii][j][2], acc[ii][j][3]));
+        for (int j = 0; j < FN; ++j) hp[j] = hpa[ii][j];
         if (hnorm) {
           float c8[FN];
 #pragma unroll
