@@ -1508,6 +1508,13 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           hpa[ii][j] = make_uint2(pack2bf(acc[ii][j][0], acc[ii][j][1]), pack2bf(acc[ii][j][2], acc[ii][j][3]));
+      // PER: materialised here (hipcc would otherwise sink the packs to their uses and keep acc live)
+      if constexpr (PER) {
+#pragma unroll
+        for (int ii = 0; ii < FM; ++ii)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) asm volatile("" : "+v"(hpa[ii][j].x), "+v"(hpa[ii][j].y));
+      }
       uint2 hw[FN];
       if (hnorm) {
         const bf16_t* wp = (const bf16_t*)ep.hn_w + hblk * ep.hn_w_stride + hhd * 128 + 4 * g4;
