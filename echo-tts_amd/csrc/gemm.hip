@@ -2100,12 +2100,16 @@ int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   ECHO_LAUNCH_CHECK();
   return 0;
 }
-// production 320-row launch: the persistent form for SwiGLU (W13: 15 / 5 tiles per CU at M = 30720 / 10240,
-// -2.5 / -3 %, profiles/r3_t320_persistent.txt) unless diag key 10 asks for one tile per workgroup; one tile
-// per workgroup for the gated residual (3 / 1 tiles per CU, K = 5888 for W2: no measurable gain) and the
-// head-norm epilogue (whose register epilogue spills in the persistent form: +22 % at M = 30720)
+// production 320-row launch: the persistent form for SwiGLU launches of at least 4 tiles per CU (W13: 15 / 5
+// tiles per CU at M = 30720 / 10240, -2.5 / -3 %, C3 +0.8 %; profiles/r3_t320_persistent.txt, r3s2_ab_t320p.txt)
+// unless diag key 10 asks for one tile per workgroup. One tile per workgroup for the blockwise W13 launch
+// (M = 7680: 2 tiles per CU, C5 -0.4 % when persistent), the gated residual (3 / 1 tiles per CU, K = 5888 for
+// W2: no measurable gain) and the head-norm epilogue (its persistent form holds ~45 dwords in scratch across
+// the K loop: +8 % at M = 30720).
 int launch_t320(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
-  return (ek_of(a) == EK_SWIGLU && !g_gemm_t320_np) ? launch_t320_sp<0, 1>(a, ep, s) : launch_t320_sp<0, 0>(a, ep, s);
+  const int64_t tiles = (int64_t)(a->M / 320) * (a->N / 256);
+  const bool per = ek_of(a) == EK_SWIGLU && !g_gemm_t320_np && tiles >= 4 * (int64_t)cu_count_cached();
+  return per ? launch_t320_sp<0, 1>(a, ep, s) : launch_t320_sp<0, 0>(a, ep, s);
 }
 
 // auto pick between 320x256 and 256x256 tiles by whole rounds of the CUs: a 320-row tile does 1.25x the work
