@@ -1238,13 +1238,15 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
 // c0-c2 -> cA + cW0 and c3 -> cW1, so the steady-state waits are vmcnt(9) (2 + 7 younger pieces).
 // Epilogue from registers, row fragment by row fragment (the residual rows of the next one in flight).
 //
-// PER = 1 (persistent; production for SwiGLU, see launch_t320): one workgroup per CU walks tiles blockIdx.x, + gridDim.x, ... (gridDim.x a
-// multiple of 8, so t & 7 stays the XCD of the block-id map); after a tile's K loop the next tile's prologue
-// DMA is issued BEFORE its epilogue, so the first K-tile loads of tile i+1 are in flight under the epilogue
-// math and store burst of tile i (gemm_bf16_ps_kernel's scheme). vmcnt counts loads, LDS-DMA and stores in
-// issue order: the T320_SN(EK) stores of a wave are younger than the prologue DMA, so the prologue wait and
-// both waits of K-tile 0 allow T320_SN more in flight; K-tile 1's first wait (cW1 of tile 1, issued after
-// the stores) retires them. Same K loop, same per-element K order: bitwise equal to PER = 0.
+// PER = 1 (persistent; production for SwiGLU launches of >= 4 tiles per CU, see launch_t320): one workgroup
+// per CU walks tiles blockIdx.x, + gridDim.x, ... (gridDim.x a multiple of 8, so t & 7 stays the XCD of the
+// block-id map); after a tile's K loop the next tile's prologue DMA is issued BEFORE its epilogue, so the first
+// K-tile loads of tile i+1 are in flight under the epilogue math and store burst of tile i (gemm_bf16_ps_kernel's
+// scheme). vmcnt counts loads, LDS-DMA and stores in issue order: the SN = t320_sn(EK) stores of a wave are
+// younger than the prologue DMA, so the prologue wait and both waits of K-tile 0 allow SN more in flight;
+// K-tile 1's first wait (cW1 of K-tile 1, issued after the stores) retires them. Memory operations the compiler
+// adds (spill code) are issued after the ops those waits target, so they only make the waits stricter.
+// Same K loop, same per-element K order: bitwise equal to PER = 0.
 constexpr int t320_sn(int ek) { return ek == EK_SWIGLU ? 10 : 20; }  // stores per wave per tile (FM x 2 / FM x 4)
 
 // The epilogue reads its arguments (C, M, N, the Epi fields) through an opaque copy of the kernarg pointer taken
