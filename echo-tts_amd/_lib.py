@@ -99,7 +99,13 @@ SIGNATURES = {
     "echo_rvq_encode": (i32, [i32, vp, i64, i32, i32, i32, C.POINTER(RvqWeights), vp, vp, i64, vp, vp, f32, vp,
                               i32, vp]),
     "echo_version": (C.c_char_p, []),
+    "echo_abi_version": (i32, []),
+    "echo_abi_struct_size": (i64, [i32]),
 }
+
+ABI_VERSION = 4  # include/echo_hip.h ECHO_ABI_VERSION
+# ctypes mirrors of the argument structs, by echo_abi_struct_size id
+ABI_STRUCTS = {0: "GemmArgs", 1: "AttnArgs", 2: "KVSegment", 3: "StepArgs", 4: "RvqWeights"}
 
 _lib = None
 
@@ -116,6 +122,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)  # AttributeError if a declared symbol is missing
         fn.restype, fn.argtypes = res, args
+    check_abi(lib)
     _lib = lib
     # A/B measurements only: ECHO_GEMM_DIAG="key=value,..." -> echo_gemm_set_diag (keys: echo_hip.h)
     for kv in filter(None, os.environ.get("ECHO_GEMM_DIAG", "").split(",")):
@@ -123,6 +130,18 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         if lib.echo_gemm_set_diag(k, v) != 0:
             raise RuntimeError(f"ECHO_GEMM_DIAG: echo_gemm_set_diag({k}, {v}) failed")
     return lib
+
+
+def check_abi(lib) -> None:
+    """Refuse a library whose argument structs differ from these ctypes mirrors (a library built from
+    another header revision would read fields past the end of a shorter struct)."""
+    v = lib.echo_abi_version()
+    if v != ABI_VERSION:
+        raise RuntimeError(f"libecho_hip.so ABI {v} != bindings ABI {ABI_VERSION}: rebuild the library")
+    for which, name in ABI_STRUCTS.items():
+        n, want = lib.echo_abi_struct_size(which), C.sizeof(globals()[name])
+        if n != want:
+            raise RuntimeError(f"libecho_hip.so sizeof({name}) = {n}, bindings {want}: rebuild the library")
 
 
 _torch_loaded = False

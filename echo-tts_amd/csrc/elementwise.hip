@@ -429,6 +429,19 @@ int echo_cast_from_f32(int32_t dtype, const float* x, void* y, int64_t n, void* 
   return 0;
 }
 
-const char* echo_version(void) { return "echo_hip gfx950 r2 " __DATE__ " " __TIME__; }
+const char* echo_version(void) { return "echo_hip gfx950 r4 abi4 " __DATE__ " " __TIME__; }
+
+int32_t echo_abi_version(void) { return ECHO_ABI_VERSION; }
+
+int64_t echo_abi_struct_size(int32_t which) {
+  switch (which) {
+    case 0: return (int64_t)sizeof(EchoGemmArgs);
+    case 1: return (int64_t)sizeof(EchoAttnArgs);
+    case 2: return (int64_t)sizeof(EchoKVSegment);
+    case 3: return (int64_t)sizeof(EchoStepArgs);
+    case 4: return (int64_t)sizeof(EchoRvqWeights);
+    default: return -1;
+  }
+}
 
 }  // extern "C"

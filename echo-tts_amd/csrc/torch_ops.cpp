@@ -292,7 +292,7 @@ EchoAttnArgs attn_args(const Tensor& q, const optional<Tensor>& gate, at::Tensor
     const optional<Tensor> len = seg_len.get(i);
     if (len.has_value() && len->defined()) {
       need_dev(q, *len, "segment lens");
-      TORCH_CHECK(len->scalar_type() == at::kInt && len->numel() >= q.size(0) && len->is_contiguous(),
+      TORCH_CHECK(len->scalar_type() == at::kInt && len->numel() >= out.size(0) && len->is_contiguous(),
                   "echo_hip.joint_attention: lens must be contiguous int32 [rows]");
       s.len = (const int32_t*)len->data_ptr();
     }

@@ -43,8 +43,10 @@ def _world(group) -> Tuple[int, int]:
 def gather_rows(local: torch.Tensor, batch: int, group=None, force_collective: bool = False) -> torch.Tensor:
     """All-gather every rank's rows [stop_r - start_r, ...] into the global [batch, ...] on every rank.
 
-    Shards are padded to ceil(batch / world) rows so a single fixed-size all-gather suffices
-    (RCCL `all_gather_into_tensor`; gloo, used by the CPU tests, gathers a list on the host).
+    Shards are padded to ceil(batch / world) rows so a single fixed-size `all_gather_into_tensor`
+    suffices. Every backend runs the same code: RCCL gathers the device tensors over xGMI; gloo (the
+    CPU tests, and bench.py --dist-backend gloo) gathers host copies — so the padding, the per-rank
+    trimming and the rank order RCCL relies on are exercised by the world-size 2 / 3 gloo tests.
     A single-rank group returns `local` unless force_collective (tests: the RCCL path on one GPU)."""
     world, rank = _world(group)
     if world == 1 and not (force_collective and dist.is_available() and dist.is_initialized()):
@@ -53,13 +55,10 @@ def gather_rows(local: torch.Tensor, batch: int, group=None, force_collective: b
     pad = local.new_zeros((rows,) + tuple(local.shape[1:]))
     pad[:local.shape[0]] = local
     if dist.get_backend(group) == "gloo":
-        host = pad.cpu()
-        parts = [torch.empty_like(host) for _ in range(world)]
-        dist.all_gather(parts, host, group=group)
-        full = torch.cat(parts).to(local.device)
-    else:
-        full = local.new_empty((world * rows,) + tuple(local.shape[1:]))
-        dist.all_gather_into_tensor(full, pad, group=group)
+        pad = pad.cpu()
+    full = pad.new_empty((world * rows,) + tuple(local.shape[1:]))
+    dist.all_gather_into_tensor(full, pad, group=group)
+    full = full.to(local.device)
     keep = [full[r * rows:r * rows + (e - s)] for r, (s, e) in
             ((r, shard_range(batch, world, r)) for r in range(world))]
     return torch.cat(keep)

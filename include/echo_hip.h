@@ -290,6 +290,15 @@ int echo_rvq_encode(int32_t dtype, const void* z, int64_t ldz, int32_t rows, int
 /* Library identification (build stamp) — for load checks. */
 const char* echo_version(void);
 
+/* ABI revision of the argument structs in this header. Bumped whenever a struct's layout changes
+ * (4: EchoAttnArgs gained the trailing q_batch_mod). A binding built against an older header must
+ * refuse to run: check echo_abi_version() == ECHO_ABI_VERSION and the struct sizes below at load. */
+#define ECHO_ABI_VERSION 4
+int32_t echo_abi_version(void);
+/* sizeof() of an argument struct as this library was compiled: 0 EchoGemmArgs, 1 EchoAttnArgs,
+ * 2 EchoKVSegment, 3 EchoStepArgs, 4 EchoRvqWeights; -1 for an unknown id. */
+int64_t echo_abi_struct_size(int32_t which);
+
 #ifdef __cplusplus
 }
 #endif

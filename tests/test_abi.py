@@ -76,6 +76,25 @@ def test_struct_layouts_match_header(tmp_path):
             assert got[(cname, f)] == getattr(cls, f).offset, (cname, f)
 
 
+def test_abi_version_and_struct_sizes(lib):
+    """The library reports the header's ECHO_ABI_VERSION and its compiled struct sizes, which equal
+    the ctypes mirrors (the load-time check `_lib.check_abi`); a mismatching mirror is refused."""
+    text = open(HEADER).read()
+    want = int(re.search(r"#define ECHO_ABI_VERSION (\d+)", text).group(1))
+    assert lib.echo_abi_version() == want == L.ABI_VERSION
+    for which, name in L.ABI_STRUCTS.items():
+        assert lib.echo_abi_struct_size(which) == C.sizeof(getattr(L, name)), name
+    assert lib.echo_abi_struct_size(99) == -1
+    old = L.AttnArgs
+    try:  # the round-2 layout (no q_batch_mod): a binding with it must be refused
+        L.AttnArgs = type("AttnArgsR2", (C.Structure,), {"_fields_": old._fields_[:-1]})
+        with pytest.raises(RuntimeError, match="sizeof"):
+            L.check_abi(lib)
+    finally:
+        L.AttnArgs = old
+    L.check_abi(lib)
+
+
 def test_ops_refuse_cpu_tensors(lib):
     import torch
     from echo_tts_amd import ops

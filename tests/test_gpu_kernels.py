@@ -613,6 +613,22 @@ def test_attention_segments(dtype):
         assert rel(out, ref) < 1e-5
 
 
+def test_attention_lens_sized_to_output_rows():
+    """With q_batch_mod (out rows a multiple of q's) the kernel reads len[row] for every OUTPUT row:
+    lens sized to q's rows must be refused, lens sized to the output rows accepted."""
+    Rg, N, H = 2, 64, 2
+    q = torch.randn(Rg, N, H, 128, device=DEV).to(BF)
+    kt = torch.randn(Rg, 96, 2, H, 128, device=DEV).to(BF)
+    out = torch.empty(3 * Rg, N, H, 128, device=DEV, dtype=BF)
+    short = torch.tensor([50, 71], dtype=torch.int32, device=DEV)
+    with pytest.raises(RuntimeError, match="lens"):
+        ops.attention(q, [ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=short, batch_mod=Rg)], out=out)
+    full = torch.tensor([50, 71, 0, 0, 50, 71], dtype=torch.int32, device=DEV)
+    ops.attention(q, [ops.Segment(kt[:, :, 0], kt[:, :, 1], lens=full, batch_mod=Rg)], out=out)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out[:Rg].float()).all()
+
+
 @pytest.mark.parametrize("dtype", [BF, torch.float32])
 @pytest.mark.parametrize("L_", [160, 37])
 def test_attention_causal(dtype, L_):

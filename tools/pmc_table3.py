@@ -23,6 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("-o", default=None)
+    ap.add_argument("--workload", default="c3", help="bench.py --workload of the profiled run")
+    ap.add_argument("--batch", type=int, default=16, help="prompts per call of the profiled run")
     ap.add_argument("--calls", type=int, default=3,
                     help="sampler calls in the profiled run (tools/gpu_pmc3.sh: 1 warmup + 2 timed)")
     args = ap.parse_args()
@@ -61,7 +63,8 @@ def main():
         # bench.py divides hbm_bytes_per_call by its roofline leg's GEMM call count: a column-split GEMM
         # (two kernel launches) is one call there, as its algorithmic bytes are
         with open(args.o, "w") as f:
-            json.dump({"source": args.root, "corrections": "FETCH_SIZE*1024*2, WRITE_SIZE*1024",
+            json.dump({"source": args.root, "workload": args.workload, "batch": args.batch,
+                       "corrections": "FETCH_SIZE*1024*2, WRITE_SIZE*1024",
                        "hbm_bytes_per_launch": fam, "hbm_bytes_per_call": per_call, "calls": args.calls,
                        "kernels": out}, f, indent=1)
 
