@@ -1455,6 +1455,8 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
   return 0;
 }
 
+extern int g_policy_num, g_policy_den;  // echo_set_policy_rows (gemm.hip)
+
 namespace {
 int g_attn_split_override = -1;  // echo_attention_set_split: force nsplit (diagnostics), -1 = policy
 
@@ -1491,7 +1493,8 @@ extern "C" int32_t echo_attention_pick_split(const EchoAttnArgs* a) {
     //   160 queries, R = 1 ( 32 items): 27.9 / 21.7 / 21.0 / 21.0  -> 3-4
     // the per-workgroup prologue (Q + first K/V tile) and the partials' round trip through L2/HBM
     // (nsplit x the output in fp32) bound the gain: split only launches that leave half the CUs idle
-    const int nitems = attn_grid(a, 128), cus = cu_count();
+    // items of the launch as a one-process run of the whole batch would have them (echo_set_policy_rows)
+    const int nitems = (int)((int64_t)attn_grid(a, 128) * g_policy_num / g_policy_den), cus = cu_count();
     nsp = nitems * 2 > cus ? 1 : nitems * 8 >= cus * 3 ? 2 : nitems * 8 > cus ? 3 : 4;
     nsp = min(nsp, tiles / 3);
   }

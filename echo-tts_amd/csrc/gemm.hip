@@ -20,6 +20,9 @@
 // fp32 kernel: plain LDS-tiled FMA GEMM for the fp32 parity mode (same epilogues).
 #include "common.h"
 
+// echo_set_policy_rows (shared with attention.hip's split-KV policy)
+int g_policy_num = 1, g_policy_den = 1;
+
 namespace {
 
 constexpr int BK = 64;
@@ -475,6 +478,236 @@ gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   }
 
   gemm_epilogue<TM, TN, FM, FN, EK>(acc, lds, wid, wm, wn, lane, m0, n0, M, N, z, Cv, ldc, sC, ep);
+}
+
+// ----------------------------------------------------------------------------- small-M launches
+// gemm_bf16_sk_kernel: the decoder GEMMs of under-filled launches (B = 1 sampler steps, blockwise
+// blocks: M = 160 ... 1920 rows). There the chip is bound by what each CU pulls from L2 into LDS
+// (≈ 70-90 GB/s per CU, MI355X_MICROARCH.md "ring-gemm"/"Indexed rows") — a 64x64 tile needs 4 B per
+// 2 x 64 MAC, and a single 4-wave workgroup with one K-tile of lookahead gets well under that rate —
+// not by MFMA. So: bigger tiles, one or two workgroups per CU, an NS-stage LDS ring with NS - 1 K-tiles
+// of LDS-DMA in flight behind counted vmcnt waits, and, where the tiles alone do not reach every CU,
+// K split over gridDim.y = S workgroups (contiguous K-tile ranges [s n / S, (s + 1) n / S)).
+//   S = 1: the shared fused epilogue; same fragments, same K order as every other bf16 kernel, so the
+//          output is bitwise the one the 256x256 / 320x256 kernels give at large M.
+//   EK = EK_PARTIAL: the unit's fp32 accumulators go to the workspace slab ws[s] ([S][M][N], ld N,
+//          straight from registers: 16 B per lane), and gemm_splitk_finish_kernel sums the S slabs in
+//          order s = 0 .. S-1 and applies the epilogue.
+constexpr int EK_PARTIAL = 6;
+
+// vmcnt(n * D) for n = 0 .. 3 (counted waits need immediates)
+template <int D>
+__device__ __forceinline__ void vm_wait_stages(int n) {
+  if (n >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * D) : "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int BM, int BN, int WM, int WN, int EK, int NS>
+__global__ void __launch_bounds__(64 * WM * WN)
+gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw,
+                    void* __restrict__ Cv, int64_t ldc, int M, int N, int K, int tiles_m, int tiles_n, Epi ep) {
+  constexpr int NW = WM * WN;
+  constexpr int NT = 64 * NW;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int STAGE = (BM + BN) * BK;  // elements per ring slot
+  constexpr int DOPS = (BM + BN) * 8 / NT;  // LDS-DMA wave-instructions per slot
+  static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "staging split");
+  static_assert(NS >= 2 && NS <= 5 && DOPS * (NS - 2) <= 63, "ring depth / vmcnt range");
+  __shared__ __attribute__((aligned(16))) bf16_t lds[NS * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+
+  // block -> tile as gemm_bf16_kernel (bijective XCD remap, group-M); blockIdx.y = K split
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  constexpr int GM = 8;
+  const int grp = wg / (GM * tiles_n);
+  const int fm = grp * GM;
+  const int gm = min(tiles_m - fm, GM);
+  const int rem = wg - grp * GM * tiles_n;
+  const int tm = fm + rem % gm, tn = rem / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int S = gridDim.y, s = blockIdx.y;
+  const int nk_all = K / BK;
+  const int kb = (int)((int64_t)s * nk_all / S);
+  const int nk = (int)((int64_t)(s + 1) * nk_all / S) - kb;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // SADDR-form DMA of K-tile kb + kt into ring slot `slot` (32-bit offsets: the host checks the extents)
+  auto stage = [&](int kt, int slot) __attribute__((always_inline)) {
+    const int k0 = (kb + kt) * BK;
+    const bf16_t* abase = A + k0;
+    const bf16_t* wbase = W + k0;
+    bf16_t* dst = lds + slot * STAGE;
+#pragma unroll
+    for (int i = 0; i < BM * 8 / NT; ++i) {
+      const int rb = (i * NW + wid) * 8;
+      const int row = rb + (lane >> 3);
+      const int gc = (lane & 7) ^ ((row >> 1) & 7);
+      const uint32_t off = (uint32_t)(((int64_t)min(m0 + row, M - 1) * lda + gc * 8) * 2);
+      glds16s(abase, off, __builtin_amdgcn_readfirstlane(lds_addr_of(dst + rb * BK)));
+    }
+#pragma unroll
+    for (int i = 0; i < BN * 8 / NT; ++i) {
+      const int rb = (i * NW + wid) * 8;
+      const int row = rb + (lane >> 3);
+      const int gc = (lane & 7) ^ ((row >> 1) & 7);
+      const uint32_t off = (uint32_t)(((int64_t)min(n0 + row, N - 1) * ldw + gc * 8) * 2);
+      glds16s(wbase, off, __builtin_amdgcn_readfirstlane(lds_addr_of(dst + BM * BK + rb * BK)));
+    }
+  };
+
+  const int frow = lane & 15;
+  const int fsw = frow >> 1;
+  auto compute = [&](const bf16_t* As) __attribute__((always_inline)) {
+    const bf16_t* Bs = As + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ph = ((4 * ks + (lane >> 4)) ^ fsw) * 8;
+      bf16x8 xf[FM], wf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) xf[i] = *(const bf16x8*)(As + (wm * TM + i * 16 + frow) * BK + ph);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) wf[j] = *(const bf16x8*)(Bs + (wn * TN + j * 16 + frow) * BK + ph);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+
+  // ring: slots hold K-tiles kt mod NS; at tile kt wait for it (the up to NS - 2 younger tiles stay in
+  // flight), barrier (tile kt visible; every wave is done reading tile kt - 1's slot), then refill that
+  // slot with tile kt + NS - 1 and compute tile kt
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) stage(p, p);
+  for (int kt = 0; kt < nk; ++kt) {
+    vm_wait_stages<DOPS>(min(NS - 2, nk - 1 - kt));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < nk) stage(kt + NS - 1, (kt + NS - 1) % NS);
+    compute(lds + (kt % NS) * STAGE);
+  }
+
+  if constexpr (EK == EK_PARTIAL) {
+    // fp32 partial tile -> ws slab s: lane holds row (lane & 15) of each 16-row fragment, 4 consecutive
+    // columns 4 (lane >> 4) .. + 3 of each 16-column fragment
+    float* slab = (float*)Cv + (int64_t)s * M * ldc;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * TM + i * 16 + frow;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * TN + j * 16 + 4 * (lane >> 4);
+        if (n < N) *(f32x4*)(slab + (int64_t)m * ldc + n) = acc[i][j];
+      }
+    }
+  } else {
+    __syncthreads();  // last fragment reads done before the epilogue reuses the LDS
+    gemm_epilogue<TM, TN, FM, FN, EK>(acc, lds, wid, wm, wn, lane, m0, n0, M, N, 0, Cv, ldc, 0, ep);
+  }
+}
+
+// Sum of the S fp32 partial slabs ws[s][M][N] (order s = 0 .. S-1) + the fused epilogue of the split
+// launch, with the roundings of gemm_epilogue: one thread per 8 output columns of one row (16 B out);
+// EK_HEADNORM: the 16 threads of a (row, 128-column head) are one 16-lane row of the wave (N % 128 == 0),
+// so the sum of squares is the xor-butterfly of head_norm_rope_kernel / the fused epilogue.
+template <int EK>
+__global__ void __launch_bounds__(256)
+gemm_splitk_finish_kernel(const float* __restrict__ ws, int S, int M, int N, void* __restrict__ Cv, int64_t ldc,
+                          Epi ep) {
+  const int Nout = EK == EK_SWIGLU ? N / 2 : N;
+  const int cpr = Nout / 8;  // 8-column chunks per output row
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)M * cpr) return;
+  const int m = (int)(t / cpr), c = (int)(t - (int64_t)m * cpr);
+  const int n = c * 8;  // first output column
+  const int64_t slab = (int64_t)M * N;
+  auto sum8 = [&](int col, float (&v)[8]) __attribute__((always_inline)) {
+    const float* p = ws + (int64_t)m * N + col;
+    load8(p, v);
+    for (int k = 1; k < S; ++k) {
+      float w[8];
+      load8(p + k * slab, w);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += w[e];
+    }
+  };
+  float v[8];
+  if constexpr (EK == EK_SWIGLU) {
+    // output column j <- GEMM columns a = (j / 16) * 32 + j % 16 and b = a + 16 (w1 / w3 blocks of 16)
+    const int a0 = (n / 16) * 32 + n % 16;
+    float a[8], b[8];
+    sum8(a0, a);
+    sum8(a0 + 16, b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = rbf(silu_bf16in(rbf(a[e]))) * rbf(b[e]);
+  } else {
+    sum8(n, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = rbf(v[e]);
+  }
+  bf16_t* out = (bf16_t*)Cv + (int64_t)m * ldc + n;
+  if constexpr (EK == EK_RESID) {
+    float x[8];
+    load8((const bf16_t*)ep.aux + (int64_t)m * ep.ld_aux + n, x);
+    if (ep.gate) {
+      float g[8];
+      load8((const bf16_t*)ep.gate + n, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = rbf(g[e] * v[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = x[e] + v[e];  // store8 rounds
+  } else if constexpr (EK == EK_HEADNORM) {
+    const int hidx = n >> 7, ch = (n >> 3) & 15;
+    const int blk = hidx / ep.hn_heads, h = hidx - blk * ep.hn_heads;
+    if (blk < ep.hn_nblk) {  // uniform over the 16 lanes of the head
+      float wv[8];
+      load8((const bf16_t*)ep.hn_w + blk * ep.hn_w_stride + h * 128 + ch * 8, wv);
+      float ss = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += v[e] * v[e];
+      ss += xor_lane16<8>(ss);
+      ss += xor_lane16<4>(ss);
+      ss += xor_lane16<2>(ss);
+      ss += xor_lane16<1>(ss);
+      const float r = 1.0f / sqrtf(ss / 128.0f + ep.hn_eps);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = rbf((v[e] * r) * wv[e]);
+      if (h < ep.hn_rope_heads) {
+        const int pos = ep.hn_pos0 + ep.hn_pos_mult * (m % ep.hn_seq_len);
+        const float4* cp = (const float4*)(ep.hn_rope + ((int64_t)pos * 64 + ch * 4) * 2);
+        const float4 c0 = cp[0], c1 = cp[1];
+        const float cc[4] = {c0.x, c0.z, c1.x, c1.z};
+        const float sn[4] = {c0.y, c0.w, c1.y, c1.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x0 = v[2 * e], x1 = v[2 * e + 1];
+          v[2 * e] = (x0 * cc[e]) - (x1 * sn[e]);
+          v[2 * e + 1] = (x0 * sn[e]) + (x1 * cc[e]);
+        }
+      }
+    }
+  }
+  store8(out, v);
 }
 
 // ----------------------------------------------------------------------------- 256x256 ping-pong
@@ -2153,8 +2386,164 @@ int g_gemm_stagger = 0;  // echo_gemm_set_diag key 1
 int g_gemm_no_rowsplit = 0;  // key 3: no row-tail split of 256x256 launches (A/B)
 int g_gemm_no_ps = 0;        // key 4: the 2-phase kernel instead of the persistent one (A/B)
 int g_gemm_no_colsplit = 0;  // key 8: no column split of 320-row launches (t320_col_split; A/B)
+int g_gemm_no_splitk = 0;    // key 11: never split K (tests that compare B = 1 bitwise with B = 16 rows)
+int g_gemm_no_sk = 0;        // key 12: no small-M kernel in the auto pick (A/B)
+
+// ---- small-M kernel family (gemm_bf16_sk_kernel): configs of `tile` 1CS
+struct SkCfg { int bm, bn, wm, wn, ns; };
+constexpr SkCfg kSk[] = {
+    {0, 0, 0, 0, 0},
+    {128, 128, 2, 2, 4},  // 1: 128 KB ring, one workgroup per CU
+    {128, 64, 2, 2, 4},   // 2: 96 KB
+    {64, 64, 2, 2, 4},    // 3: 64 KB, two per CU
+    {160, 64, 2, 2, 4},   // 4: 112 KB (the blockwise block's 160 rows in one tile)
+    {64, 128, 2, 2, 4},   // 5: 96 KB
+    {128, 128, 2, 4, 4},  // 6-9: the same tiles with 8 waves (two per SIMD: one wave's fragment reads
+    {128, 64, 2, 4, 4},   //      under the other's MFMAs)
+    {64, 64, 2, 4, 4},
+    {64, 128, 2, 4, 4},
+};
+constexpr int kNumSk = 9;
+int sk_occ(int c) { return (160 * 1024) / ((kSk[c].bm + kSk[c].bn) * BK * 2 * kSk[c].ns); }
+
+// the fused epilogue straight from the unit's registers is expressible for this wave tile (gemm_epilogue's
+// row-chunk loop must divide the wave's rows); otherwise the launch goes through the finish kernel
+constexpr bool sk_direct(int tm, int tn, int ek) {
+  // SwiGLU pairs the w1 / w3 16-column blocks inside a wave: its tile needs whole pairs (tn % 32 == 0)
+  return ek == EK_SWIGLU ? (tn % 32 == 0 && tm % (64 / (tn / 16)) == 0)
+                         : (ek == EK_STORE || ek == EK_RESID) && tm % (64 / (tn / 8)) == 0;
+}
+
+// small-M path applies: bf16, one batch, no conv, a fused kind the finish kernel has, 32-bit DMA offsets
+bool sk_ok(const EchoGemmArgs* a) {
+  const int ek = ek_of(a);
+  if (a->dtype != ECHO_BF16 || a->batch != 1 || a->conv_taps > 0) return false;
+  if (ek != EK_STORE && ek != EK_SWIGLU && ek != EK_RESID && ek != EK_HEADNORM) return false;
+  if (ek == EK_HEADNORM && (a->N % 128 || a->hn_heads <= 0)) return false;
+  if (ek == EK_SWIGLU && a->N % 32) return false;
+  if (!ns3_ok(a) || a->K < 128) return false;
+  if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C) & 15) return false;
+  if (ek == EK_RESID && ((((uintptr_t)a->aux | (uintptr_t)a->gate) & 15) || a->ld_aux % 8)) return false;
+  return true;
+}
+
+bool sk_partial(int c, int S, int ek) {
+  const int tm = kSk[c].bm / kSk[c].wm, tn = kSk[c].bn / kSk[c].wn;
+  return S > 1 || ek == EK_HEADNORM || !sk_direct(tm, tn, ek);
+}
+
+int64_t sk_ws_bytes(const EchoGemmArgs* a, int c, int S) {
+  return sk_partial(c, S, ek_of(a)) ? (int64_t)S * a->M * a->N * 4 : 0;
+}
+
+// Cost model of a small-M launch (seconds), calibrated on MI355X (tools/bench_gemm.py --sk sweep,
+// profiles/r4_sk_sweep.txt): each unit pulls (BM + BN) x K/S x 2 B into LDS at ≈ SK_RCU per CU (shared by
+// the co-resident units) or is MFMA-bound at SK_PCU, plus a fixed per-unit cost; a split / partial launch
+// adds the fp32 slabs' round trip and the finish kernel.
+constexpr double SK_RCU = 80e9, SK_PCU = 7.5e12, SK_T0 = 1.5e-6, SK_TFIN = 2.0e-6, SK_BWFIN = 4.0e12;
+double sk_cost(const EchoGemmArgs* a, int c, int S, int64_t M, int cus) {
+  const SkCfg& k = kSk[c];
+  const int64_t tiles = ((M + k.bm - 1) / k.bm) * ((a->N + k.bn - 1) / k.bn);
+  const int occ = sk_occ(c);
+  const double units = (double)tiles * S;
+  const double rounds = ceil(units / ((double)cus * occ));
+  const double kk = (double)a->K / S;
+  const double t_in = (double)(k.bm + k.bn) * kk * 2 * occ / SK_RCU;
+  const double t_mf = 2.0 * k.bm * k.bn * kk * occ / SK_PCU;
+  double t = rounds * (fmax(t_in, t_mf) + SK_T0);
+  if (sk_partial(c, S, ek_of(a)))
+    t += SK_TFIN + (double)S * M * a->N * 4 * 2 / SK_BWFIN;
+  return t;
+}
+
+// the small-M plan: config and K split from the POLICY rows (echo_set_policy_rows: the rows the launch
+// would have in a one-process run of the whole batch), so that the split — the only choice that changes
+// the summation order — is the one-process choice on every rank
+int64_t policy_rows(int64_t rows) { return rows * g_policy_num / g_policy_den; }
+
+bool sk_plan(const EchoGemmArgs* a, bool allow_split, int* cfg, int* split) {
+  if (g_gemm_no_sk || !sk_ok(a)) return false;
+  const int64_t Mp = policy_rows(a->M);
+  // only launches the large tiles leave under-filled (pick_tile takes a small config there)
+  if (pick_tile((int)std::min<int64_t>(Mp, 1 << 30), a->N, a->K, 1) == 1) return false;
+  const int cus = cu_count_cached();
+  const int nk = a->K / BK;
+  double best = 1e300;
+  int bc = 0, bs = 1;
+  for (int c = 1; c <= kNumSk; ++c) {
+    for (int S = 1; S <= 8; ++S) {
+      if (S > 1 && (!allow_split || g_gemm_no_splitk || nk < 2 * S)) break;
+      const double e = sk_cost(a, c, S, Mp, cus);
+      if (e < best * 0.999) { best = e; bc = c; bs = S; }
+    }
+  }
+  *cfg = bc;
+  *split = bs;
+  return bc > 0;
+}
 
 }  // namespace
+
+template <int BM, int BN, int WM, int WN, int NS, int EK>
+int launch_sk_direct(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  if constexpr (sk_direct(TM, TN, EK)) {
+    const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;
+    hipLaunchKernelGGL((gemm_bf16_sk_kernel<BM, BN, WM, WN, EK, NS>), dim3(tm * tn, 1), dim3(64 * WM * WN), 0, s,
+                       (const bf16_t*)a->A, a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm,
+                       tn, ep);
+    ECHO_LAUNCH_CHECK();
+    return 0;
+  } else {
+    return ECHO_EINVAL;
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int NS>
+int launch_sk(const EchoGemmArgs* a, const Epi& ep, int S, void* ws, hipStream_t s) {
+  const int ek = ek_of(a);
+  const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;
+  if (!(S > 1 || ek == EK_HEADNORM || !sk_direct(BM / WM, BN / WN, ek))) {
+    switch (ek) {
+      case EK_STORE: return launch_sk_direct<BM, BN, WM, WN, NS, EK_STORE>(a, ep, s);
+      case EK_SWIGLU: return launch_sk_direct<BM, BN, WM, WN, NS, EK_SWIGLU>(a, ep, s);
+      case EK_RESID: return launch_sk_direct<BM, BN, WM, WN, NS, EK_RESID>(a, ep, s);
+      default: return ECHO_EINVAL;
+    }
+  }
+  hipLaunchKernelGGL((gemm_bf16_sk_kernel<BM, BN, WM, WN, EK_PARTIAL, NS>), dim3(tm * tn, S), dim3(64 * WM * WN), 0, s,
+                     (const bf16_t*)a->A, a->lda, (const bf16_t*)a->W, a->ldw, ws, (int64_t)a->N, a->M, a->N, a->K,
+                     tm, tn, ep);
+  ECHO_LAUNCH_CHECK();
+  const int nout = ek == EK_SWIGLU ? a->N / 2 : a->N;
+  const int64_t threads = (int64_t)a->M * (nout / 8);
+  const dim3 g((unsigned)((threads + 255) / 256));
+  const float* w = (const float*)ws;
+  switch (ek) {
+    case EK_STORE: hipLaunchKernelGGL(gemm_splitk_finish_kernel<EK_STORE>, g, dim3(256), 0, s, w, S, a->M, a->N, a->C, a->ldc, ep); break;
+    case EK_SWIGLU: hipLaunchKernelGGL(gemm_splitk_finish_kernel<EK_SWIGLU>, g, dim3(256), 0, s, w, S, a->M, a->N, a->C, a->ldc, ep); break;
+    case EK_RESID: hipLaunchKernelGGL(gemm_splitk_finish_kernel<EK_RESID>, g, dim3(256), 0, s, w, S, a->M, a->N, a->C, a->ldc, ep); break;
+    case EK_HEADNORM: hipLaunchKernelGGL(gemm_splitk_finish_kernel<EK_HEADNORM>, g, dim3(256), 0, s, w, S, a->M, a->N, a->C, a->ldc, ep); break;
+    default: return ECHO_EINVAL;
+  }
+  ECHO_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_sk_cfg(const EchoGemmArgs* a, const Epi& ep, int c, int S, void* ws, hipStream_t s) {
+  switch (c) {
+    case 1: return launch_sk<128, 128, 2, 2, 4>(a, ep, S, ws, s);
+    case 2: return launch_sk<128, 64, 2, 2, 4>(a, ep, S, ws, s);
+    case 3: return launch_sk<64, 64, 2, 2, 4>(a, ep, S, ws, s);
+    case 4: return launch_sk<160, 64, 2, 2, 4>(a, ep, S, ws, s);
+    case 5: return launch_sk<64, 128, 2, 2, 4>(a, ep, S, ws, s);
+    case 6: return launch_sk<128, 128, 2, 4, 4>(a, ep, S, ws, s);
+    case 7: return launch_sk<128, 64, 2, 4, 4>(a, ep, S, ws, s);
+    case 8: return launch_sk<64, 64, 2, 4, 4>(a, ep, S, ws, s);
+    case 9: return launch_sk<64, 128, 2, 4, 4>(a, ep, S, ws, s);
+    default: return ECHO_EINVAL;
+  }
+}
 
 extern int g_adaln_blocks;  // elementwise.hip
 
@@ -2170,6 +2559,8 @@ extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   else if (key == 8) g_gemm_no_colsplit = value != 0;
   else if (key == 9) g_adaln_blocks = value;
   else if (key == 10) g_gemm_t320_np = value != 0;
+  else if (key == 11) g_gemm_no_splitk = value != 0;
+  else if (key == 12) g_gemm_no_sk = value != 0;
   else return ECHO_EINVAL;
   return 0;
 }
@@ -2179,7 +2570,28 @@ extern "C" int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batc
   return t == 1 ? 13 : t;
 }
 
-extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
+extern "C" int echo_set_policy_rows(int32_t num, int32_t den) {
+  if (num <= 0 || den <= 0 || num < den) return ECHO_EINVAL;
+  g_policy_num = num;
+  g_policy_den = den;
+  return 0;
+}
+
+extern "C" int64_t echo_gemm_ws_bytes(const EchoGemmArgs* a) {
+  if (!a || a->M <= 0 || a->N <= 0 || a->K <= 0 || a->K % BK) return 0;
+  if (a->tile >= 110 && a->tile <= 199) {
+    const int c = (a->tile / 10) % 10, S = a->tile % 10;
+    if (c < 1 || c > kNumSk || S < 1 || !sk_ok(a)) return 0;
+    return sk_ws_bytes(a, c, S);
+  }
+  int c = 0, S = 1;
+  if (a->tile == 0 && sk_plan(a, true, &c, &S)) return sk_ws_bytes(a, c, S);
+  return 0;
+}
+
+extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) { return echo_gemm_ws(a, nullptr, 0, stream); }
+
+extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, void* stream) {
   if (!a || !a->A || !a->W || !a->C) return ECHO_EINVAL;
   if (a->M <= 0 || a->N <= 0 || a->K <= 0 || a->batch <= 0) return ECHO_ESHAPE;
   if (a->K % 64 || a->N % 16 || a->lda % 8 || a->ldw % 8 || a->ldc % 8) return ECHO_EALIGN;
@@ -2207,6 +2619,24 @@ extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) {
          a->epilogue, a->act, a->out_div,
          a->hn_w, a->hn_w_stride, a->hn_rope, a->hn_heads, a->hn_nblk, a->hn_rope_heads, a->hn_seq_len,
          a->hn_pos0, a->hn_pos_mult, a->hn_eps, 0, a->act_alpha, a->conv_c, a->conv_taps, a->conv_dil};
+  // small-M family (gemm_bf16_sk_kernel): forced (`tile` 1CS) or the auto pick of under-filled launches
+  if (a->tile >= 110 && a->tile <= 199) {
+    const int c = (a->tile / 10) % 10, S = a->tile % 10;
+    if (c < 1 || c > kNumSk || S < 1 || !sk_ok(a) || a->K / BK < S) return ECHO_EINVAL;
+    const int64_t need = sk_ws_bytes(a, c, S);
+    if (need > 0 && (!ws || (uintptr_t)ws % 16 || ws_bytes < need)) return ECHO_EINVAL;
+    return launch_sk_cfg(a, ep, c, S, ws, (hipStream_t)stream);
+  }
+  if (a->tile == 0) {
+    int c = 0, S = 1;
+    if (sk_plan(a, ws != nullptr, &c, &S)) {
+      const int64_t need = sk_ws_bytes(a, c, S);
+      if (need == 0 || (ws && (uintptr_t)ws % 16 == 0 && ws_bytes >= need))
+        return launch_sk_cfg(a, ep, c, S, ws, (hipStream_t)stream);
+      if (sk_plan(a, false, &c, &S) && sk_ws_bytes(a, c, S) == 0)  // the best plan without a workspace
+        return launch_sk_cfg(a, ep, c, S, nullptr, (hipStream_t)stream);
+    }
+  }
   if (a->tile == 14 || a->tile == 18) ep.stagger = g_gemm_stagger;
   if (a->tile == 15) ep.epi = 99;  // diagnostic: no epilogue
   int t = a->tile > 0 ? a->tile : pick_tile(a->M, a->N, a->K, a->batch);

@@ -209,7 +209,15 @@ void gemm_launch(const Tensor& a, const Tensor& w, const Tensor& out, const opti
     g.hn_eps = (float)hn_eps;
   }
   c10::DeviceGuard guard(a.device());
-  check_rc(echo_gemm(&g, stream_of(a)), "echo_hip.gemm");
+  // under-filled launches may split K (echo_gemm_ws_bytes > 0): the fp32 partial slabs come from the
+  // caching allocator (graph-private pool under hipGraph capture)
+  const int64_t wsb = echo_gemm_ws_bytes(&g);
+  if (wsb > 0) {
+    Tensor ws = at::empty({(wsb + 3) / 4}, a.options().dtype(at::kFloat));
+    check_rc(echo_gemm_ws(&g, ws.data_ptr(), wsb, stream_of(a)), "echo_hip.gemm");
+  } else {
+    check_rc(echo_gemm(&g, stream_of(a)), "echo_hip.gemm");
+  }
 }
 
 Tensor gemm(const Tensor& a, const Tensor& w, const optional<Tensor>& bias, int64_t epilogue,

@@ -21,6 +21,7 @@ from typing import List, Optional, Tuple
 import torch
 import torch.distributed as dist
 
+from . import ops
 from .inference import sample_with_noise
 from .inference_blockwise import blockwise_with_noise
 
@@ -75,13 +76,12 @@ def sample_euler_cfg_sharded(model, speaker_latent: torch.Tensor, speaker_mask: 
     rank r samples prompts shard_range(B, G, r) with rows of the global x_T draw. Returns the
     global [B, N, 80] latents on every rank (gather=True) or this rank's rows.
 
-    Equality with one process sampling all B prompts: every kernel treats prompts independently,
-    except that the attention's split-KV count is chosen from the launch's row count
-    (`echo_attention_pick_split`: only launches with fewer (row, head, 128-query) items than half
-    the CUs split, e.g. 1 prompt per rank at 640 latents). Where a rank's launches pick the same
-    count as the one-process run (at 640 latents: >= 2 prompts per rank and the one-process batch
-    as well) the gathered batch is bitwise equal; otherwise it differs only in the fp32 summation
-    order over keys (fp32-close; bf16 outputs within the kernel's rounding)."""
+    Equality with one process sampling all B prompts: every kernel treats prompts independently;
+    the only choices that depend on a launch's row count and change a summation order — the GEMM's
+    K split and the attention's split-KV count for under-filled launches — are taken for the rows the
+    launch has in the one-process run (`ops.policy_rows(B, shard size)`, echo_set_policy_rows). So
+    the gathered batch is bitwise the one-process result at every world size, 1 prompt per rank
+    included (tests/test_gpu_distributed.py)."""
     world, rank = _world(group)
     B = text_input_ids.shape[0]
     N = 640 if sequence_length is None else sequence_length
@@ -89,8 +89,9 @@ def sample_euler_cfg_sharded(model, speaker_latent: torch.Tensor, speaker_mask: 
     noise = torch.randn((B, N, 80), device=model.device, dtype=torch.float32, generator=rng)
     s, e = shard_range(B, world, rank)
     if e > s:
-        lat = sample_with_noise(model, speaker_latent[s:e], speaker_mask[s:e], text_input_ids[s:e],
-                                text_mask[s:e], noise[s:e], **sampler_kw)
+        with ops.policy_rows(B, e - s):
+            lat = sample_with_noise(model, speaker_latent[s:e], speaker_mask[s:e], text_input_ids[s:e],
+                                    text_mask[s:e], noise[s:e], **sampler_kw)
     else:
         lat = noise[:0].clone()
     return gather_rows(lat, B, group, force_collective) if gather else lat
@@ -116,8 +117,9 @@ def sample_blockwise_sharded(model, speaker_latent: torch.Tensor, speaker_mask: 
 
     if e > s:
         cont = None if continuation_latent is None else continuation_latent[s:e]
-        lat = blockwise_with_noise(model, speaker_latent[s:e], speaker_mask[s:e], text_input_ids[s:e],
-                                   text_mask[s:e], noise, block_sizes, continuation_latent=cont, **sampler_kw)
+        with ops.policy_rows(B, e - s):
+            lat = blockwise_with_noise(model, speaker_latent[s:e], speaker_mask[s:e], text_input_ids[s:e],
+                                       text_mask[s:e], noise, block_sizes, continuation_latent=cont, **sampler_kw)
     else:
         start0 = 0 if continuation_latent is None else continuation_latent.shape[1]
         lat = torch.empty((0, start0 + sum(block_sizes), 80), device=model.device)

@@ -456,7 +456,9 @@ def _split_sizes(B: int, N: int) -> Optional[Tuple[int, int]]:
 
 
 def plan_key(B, N, Tc, Pc, sched: Schedule, kv_scale, kv_max_layers):
-    return (B, N, Tc, Pc, sched, kv_scale, kv_max_layers)
+    # the split policy (ops.policy_rows) is part of the key: a captured graph holds the split-K / split-KV
+    # choices made under it
+    return (B, N, Tc, Pc, sched, kv_scale, kv_max_layers, ops.current_policy_rows())
 
 
 def _cached(model: EchoDiTHip, key, make):

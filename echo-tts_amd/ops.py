@@ -148,6 +148,50 @@ def attention_split(nsplit: int):
 
 
 @contextlib.contextmanager
+def gemm_no_splitk():
+    """Inside the block no GEMM splits K (echo_gemm_set_diag key 11): every launch sums K in the one
+    order all unsplit kernels share, so B = 1 rows equal B = 16 rows bitwise (tests). Outside it the
+    small-M plan may split K of under-filled launches (echo_gemm_ws)."""
+    rc = lib().echo_gemm_set_diag(11, 1)
+    if rc:
+        raise RuntimeError(f"echo_gemm_set_diag(11, 1) failed: {rc}")
+    try:
+        yield
+    finally:
+        lib().echo_gemm_set_diag(11, 0)
+
+
+@contextlib.contextmanager
+def policy_rows(num: int, den: int):
+    """Split decisions (GEMM split-K, attention split-KV) taken for num / den times each launch's rows
+    (echo_set_policy_rows): a rank running den of a sharded batch's num prompts makes the choices of a
+    one-process run of the whole batch, so its rows are bitwise those of that run."""
+    global _POLICY
+    import math
+    g = math.gcd(int(num), int(den))
+    num, den = int(num) // g, int(den) // g
+    prev = _POLICY
+    rc = lib().echo_set_policy_rows(num, den)
+    if rc:
+        raise RuntimeError(f"echo_set_policy_rows({num}, {den}) failed: {rc}")
+    _POLICY = (num, den)
+    try:
+        yield
+    finally:
+        lib().echo_set_policy_rows(*prev)
+        _POLICY = prev
+
+
+_POLICY = (1, 1)
+
+
+def current_policy_rows() -> Tuple[int, int]:
+    """The (num, den) set by the innermost `policy_rows` block ((1, 1) outside): part of a captured
+    plan's identity, since its graph holds the split choices taken under it."""
+    return _POLICY
+
+
+@contextlib.contextmanager
 def attention_pipeline(on: bool):
     """Route non-causal bf16 attention launches to the asm-owned pipelined kernel (True, the default)
     or to the compiler-scheduled kernel (False) inside the block (A/B tests and measurements)."""

@@ -85,6 +85,23 @@ int echo_gemm(const EchoGemmArgs* args, void* stream);
 /* Tile configuration echo_gemm picks for a shape when args->tile == 0 (1..5). */
 int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch);
 
+/* Under-filled launches (the B = 1 and blockwise decoder GEMMs, M <= a few thousand rows) can split K
+ * over S workgroups that each store an fp32 partial tile; a second kernel sums the S partials in order
+ * and applies the fused epilogue. That needs a device workspace of echo_gemm_ws_bytes(args) bytes
+ * (0: the plan for these arguments does not split K) passed to echo_gemm_ws. echo_gemm(args, stream)
+ * is echo_gemm_ws(args, NULL, 0, stream): it never splits K. Same results as echo_gemm except that a
+ * split launch sums K in S contiguous partial sums (fp32; the unsplit kernels all share one K order).
+ * The workspace is only touched by the launched kernels (stream-ordered, capturable). */
+int64_t echo_gemm_ws_bytes(const EchoGemmArgs* args);
+int echo_gemm_ws(const EchoGemmArgs* args, void* ws, int64_t ws_bytes, void* stream);
+
+/* Split decisions (GEMM split-K here, split-KV in echo_attention_pick_split) depend on the launch's
+ * row count. A process that runs `den` of the `num` prompts of a sharded batch (echo_tts_amd.distributed)
+ * sets num / den so that every such decision is taken for the rows the whole batch would have in one
+ * process: each rank then runs the same kernels, with the same summation order, as a one-process run of
+ * the whole batch (bitwise-equal gathered output). 1 / 1 (default) = decide on the launch's own rows. */
+int echo_set_policy_rows(int32_t num, int32_t den);
+
 /* Diagnostic knobs for tools/bench_gemm.py (not used by the product path). key 1: start delay
  * between the 8 first-round workgroup groups of an XCD for `tile` = 14 (the 256x256 kernel with
  * staggered tile rounds), in 10 ns ticks; also the persistent kernel's group-M height for
@@ -98,7 +115,10 @@ int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch);
  * column split of auto-picked 320-row launches (W13: 320-row tiles on whole rounds of tile columns, the
  * rest on the persistent 256x256 kernel); key 9: block cap of the wave-per-row AdaLN kernel (0 = 8192);
  * key 10: 1 = one 320-row tile per workgroup instead of the persistent 320-row SwiGLU kernel (`tile` 22 / 23
- * force either form for any epilogue) (A/B timing, tools/bench_streams.py --diag; all bitwise-equal). */
+ * force either form for any epilogue) (A/B timing, tools/bench_streams.py --diag; all bitwise-equal).
+ * key 11: 1 = never split K in echo_gemm_ws (the B = 1 runs that tests compare bitwise with B = 16 rows);
+ * key 12: 1 = no small-M kernel in the auto pick (the round-3 small tiles; A/B).
+ * `tile` 1CS (C = small-M config 1..6, S = split 1..9) forces a small-M launch (tools/bench_gemm.py). */
 int echo_gemm_set_diag(int32_t key, int32_t value);
 
 /* One key/value segment of the joint attention (model.py:246-253): rows of

@@ -42,8 +42,8 @@ BF = torch.bfloat16
 REPORT = []
 
 
-ROW_OP, SDPA, BLOCK = "row-op", "sdpa", "block"
-BUDGET = {ROW_OP: (0.05, 0.999), SDPA: (1.25, 0.6), BLOCK: (0.75, None)}
+ROW_OP, SDPA, SDPA_SPLIT, BLOCK = "row-op", "sdpa", "sdpa-split", "block"
+BUDGET = {ROW_OP: (0.05, 0.999), SDPA: (1.25, 0.6), SDPA_SPLIT: (1.25, None), BLOCK: (0.75, None)}
 
 
 def check(tag, ours, ref, e_ref, kind=ROW_OP):
@@ -64,7 +64,7 @@ def check(tag, ours, ref, e_ref, kind=ROW_OP):
 
 @pytest.fixture(scope="module")
 def m16():
-    S = W.synthetic_state_dict(E.FULL, dtype=BF, include_latent=False)
+    S = W.synthetic_state_dict(E.FULL, dtype=BF, include_latent=True)
     return EchoDiTHip(E.FULL, S, device=DEV, dtype=BF)
 
 
@@ -393,3 +393,140 @@ def test_nfe_attribution_reference_sdpa_rounding(m16, gb, monkeypatch):
         print(line)
         REPORT.append(line)
         assert 0.75 * e_prod <= e <= 1.25 * e_prod, i
+
+
+# ------------------------------------------------------------------------------ C5 latent segment (block 2)
+# Fixture: tests/golden/full_c5_blocks.safetensors (make_golden_blocks_c5.py): the reference's bf16 C5 run
+# (/root/reference/inference_blockwise.py:14-123) at the first NFE of block 2 — start_pos 320, a latent prefix
+# of 320 latents (80 visible patches of 160: mask 4j < start_pos, model.py:241-244), speaker KV scaled by 1.5.
+
+
+@pytest.fixture(scope="module")
+def gc5():
+    return load_golden("full_c5_blocks"), load_meta("full_c5_blocks")
+
+
+def _ada5(g, i, a):
+    return tuple(d(g[f"ada.l{i}.{a}.{c}"]) for c in ("shift", "scale1", "gate"))
+
+
+def test_c5_latent_state_and_kv_projection(m16, gc5):
+    """latent_norm of the reference's last latent-encoder output, and the 24-layer latent K/V projection
+    (wk_latent / wv_latent, k_norm, half RoPE at positions 4j: model.py:283-293,623-636) of the reference's
+    normed latent state, on the 80 patches visible at start_pos 320."""
+    g, meta = gc5
+    e_ref = meta["e_ref"]
+    vis = meta["latent_visible"]
+    x = d(g["lat.norm_in"])
+    st = ops.rmsnorm(x.view(x.shape[1], -1), m16.latent_norm, E.FULL.norm_eps)
+    check("latent state (RMSNorm)", st.view(x.shape), g["lat.state"], e_ref["lat.state"])
+    ref_st = d(g["lat.state"])[0, :vis].contiguous()
+    kv = m16._kv_project(ref_st, m16.w_kv_latent, 1, vis, True)   # [1, vis, L, 2, H, 128]
+    for layer in meta["kv_layers"]:
+        for j, name in ((0, "k"), (1, "v")):
+            key = f"kv.latent.{layer}.{name}"
+            check(f"latent KV layer {layer} {name} (RoPE at 4j)", kv[:, :, layer, j], g[key], e_ref[key])
+
+
+def _c5_segs(g, meta, i):
+    """[latent | text | speaker] segments of layer i as the reference's SDPA consumed them (CFG rows)."""
+    vis, tv, sv = meta["latent_visible"], meta["text_valid"], meta["speaker_valid"]
+    ll = torch.tensor([vis] * 3, dtype=torch.int32, device=DEV)
+    tl = torch.tensor([tv, 0, tv], dtype=torch.int32, device=DEV)
+    sl = torch.tensor([sv, sv, 0], dtype=torch.int32, device=DEV)
+    return [ops.Segment(d(g[f"kv.latent.{i}.k"]), d(g[f"kv.latent.{i}.v"]), lens=ll, batch_mod=1),
+            ops.Segment(d(g[f"seg.b{i}.text.k"]), d(g[f"seg.b{i}.text.v"]), lens=tl, batch_mod=1),
+            ops.Segment(d(g[f"seg.b{i}.speaker.k"]), d(g[f"seg.b{i}.speaker.v"]), lens=sl, batch_mod=1)]
+
+
+def test_c5_decoder_block0_subops(m16, gc5):
+    """Block 0 of block 2's first (CFG) NFE, op by op, each fed the reference's own bf16 input: the RoPE
+    offset start_pos + i of q and k (model.py:229-232), and the joint attention over [self | latent | text |
+    speaker] with the latent mask 4j < start_pos (model.py:237-261), then the rest of the block."""
+    g, meta = gc5
+    e_ref = meta["e_ref"]
+    sp = meta["start_pos"]
+    w0, w1 = meta["win"]
+    nw = w1 - w0
+    cfg = E.FULL
+    D, H, eps = cfg.model_size, cfg.num_heads, cfg.norm_eps
+    lay = m16.layers[0]
+    sub = lambda k: g[f"sub.{k}"]  # noqa: E731
+    er = lambda k: e_ref[f"sub.{k}"]  # noqa: E731
+    sh_a, s1_a, g_a = _ada5(g, 0, "a")
+    sh_m, s1_m, g_m = _ada5(g, 0, "m")
+    R = sub("gated").shape[0]
+    N = g["dec.b0.in"].shape[1]
+    h_full = d(g["dec.b0.in"]).view(N, D)
+
+    xa = ops.adaln_modulate(h_full[w0:w1].contiguous(), sh_a, s1_a, eps)
+    check("C5 AdaLN (attention)", xa.view(1, nw, D), sub("xa")[:1], er("xa"))
+    # q on the window: RoPE positions start_pos + w0 + i; k / v on all N tokens: start_pos + i
+    hn = lambda pos0, L_: ops.HeadNorm(lay.qk_norm, H, 2, eps, w_stride=H * 128, rope=m16.rope,  # noqa: E731
+                                       rope_heads=H // 2, seq_len=L_, pos0=pos0)
+    qkvg = ops.gemm(d(sub("xa")[:1]).view(nw, D), lay.wqkvg, head_norm=hn(sp + w0, nw)).view(1, nw, 4, H, 128)
+    check("C5 q (wq + q_norm + RoPE at start_pos + i)", qkvg[:, :, 0], sub("q"), er("q"))
+    check("C5 gate projection", qkvg[:, :, 3].reshape(1, nw, D), sub("gate_lin"), er("gate_lin"))
+    xa_all = ops.adaln_modulate(h_full, sh_a, s1_a, eps)
+    kv_all = ops.gemm(xa_all, lay.wqkvg, head_norm=hn(sp, N)).view(1, N, 4, H, 128)
+    check("C5 k (wk + k_norm + RoPE at start_pos + i)", kv_all[:, :, 1], sub("k"), er("k"))
+    check("C5 v (wv)", kv_all[:, :, 2], sub("v"), er("v"))
+
+    segs = [ops.Segment(d(sub("k")), d(sub("v")))] + _c5_segs(g, meta, 0)
+    q = d(sub("q"))
+    gate = d(sub("gate_lin")).view(1, nw, H, 128)
+    out = torch.empty((R, nw, H, 128), device=DEV, dtype=BF)
+    with ops.attention_split(1):
+        ops.attention(q, segs, out=out)
+        check("C5 SDPA [self | latent | text | speaker] (no gate)", out, sub("sdpa"), er("sdpa"), SDPA)
+        ops.attention(q, segs, out=out, gate=gate)
+    check("C5 SDPA * sigmoid(gate)", out.view(R, nw, D), sub("gated"), er("gated"), SDPA)
+    # the production split-KV form of this (under-filled) launch: within the SDPA budget too
+    ops.attention(q, segs, out=out, gate=gate)
+    check("C5 SDPA * sigmoid(gate), split-KV", out.view(R, nw, D), sub("gated"), er("gated"), SDPA_SPLIT)
+
+    gated = d(sub("gated")).view(R * nw, D)
+    check("C5 wo", ops.gemm(gated, lay.wo).view(R, nw, D), sub("attn_out"), er("attn_out"))
+    h = h_full[w0:w1].repeat(R, 1)
+    ops.gemm(gated, lay.wo, out=h, epilogue=L.EPI_RESID, aux=h, gate=g_a)
+    check("C5 wo + gated residual", h.view(R, nw, D), sub("h_attn"), er("h_attn"))
+    h_attn = d(sub("h_attn")).view(R * nw, D)
+    xm = ops.adaln_modulate(h_attn, sh_m, s1_m, eps)
+    check("C5 AdaLN (MLP)", xm.view(R, nw, D), sub("xm"), er("xm"))
+    u = ops.gemm(d(sub("xm")).view(R * nw, D), lay.w13, epilogue=L.EPI_SWIGLU)
+    check("C5 w1/w3 + SwiGLU", u.view(R, nw, -1), sub("u"), er("u"))
+    uu = d(sub("u")).view(R * nw, -1)
+    check("C5 w2", ops.gemm(uu, lay.w2).view(R, nw, D), sub("mlp_out"), er("mlp_out"))
+    ops.gemm(uu, lay.w2, out=h_attn, epilogue=L.EPI_RESID, aux=h_attn, gate=g_m)
+    check("C5 w2 + gated residual (= block 0 output)", h_attn.view(R, nw, D), g["dec.b0.out"], e_ref["dec.b0.out"])
+
+
+@pytest.mark.parametrize("i", [0, 23])
+def test_c5_decoder_block(m16, gc5, i):
+    """A whole TransformerBlock of block 2's CFG NFE (start_pos 320, latent segment of 80 visible patches)
+    through the production layer (`decoder_layer`, layer-0 CFG sharing for block 0) on the reference's
+    block input, with the reference's AdaLN vectors and K/V segments."""
+    g, meta = gc5
+    cfg = E.FULL
+    D = cfg.model_size
+    w0, w1 = meta["win"]
+    x = g[f"dec.b{i}.in"]
+    N = x.shape[1]
+    ref_out = g[f"dec.b{i}.out"]
+    R = ref_out.shape[0]
+    tab = torch.zeros((2 * cfg.num_layers, 3, D), device=DEV, dtype=BF)
+    for a, ai in (("a", 0), ("m", 1)):
+        for c, t in enumerate(_ada5(g, i, a)):
+            tab[2 * i + ai, c] = t
+    segs = _c5_segs(g, meta, i)
+    ws = m16.workspace(R * N)
+    ws.h.view(R, N, D).copy_(d(x).expand(R, N, D))
+    share = 3 if i == 0 else 1
+    m16.decoder_layer(ws, i, R, N, tab, segs, meta["start_pos"], share_copies=share)
+    ours = ws.h.view(R, N, D)[:, w0:w1].clone()
+    check(f"C5 decoder block {i}, block 2 NFE 0 (start_pos 320)", ours, ref_out, meta["e_ref"][f"dec.b{i}.out"],
+          BLOCK)
+    if share > 1:
+        ws.h.view(R, N, D).copy_(d(x).expand(R, N, D))
+        m16.decoder_layer(ws, i, R, N, tab, segs, meta["start_pos"], share_copies=1)
+        assert torch.equal(ws.h.view(R, N, D)[:, w0:w1], ours)

@@ -135,3 +135,79 @@ def test_rccl_gather_single_rank_matches_unsharded():
     full = sample_euler_cfg_independent_guidances(m, spk, sm, ids, tm, 11, sequence_length=N, **KW).cpu()
     full_blk = sample_blockwise_euler_cfg_independent_guidances(m, spk, sm, ids, tm, 12, BLOCKS, **KW_BLK).cpu()
     assert torch.equal(lat, full) and torch.equal(blk, full_blk)
+
+
+FULL_KW = dict(KW, num_steps=4)
+
+
+def _full_worker(rank, world, port, q, policy):
+    """Full-size model (random init), 640 latents, one prompt per rank: the shapes where a 1-prompt launch
+    and the 2-prompt launch choose different splits (attention: 80 vs 160 items of the plain step)."""
+    import sys
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    import echo_tts_amd as E
+    from echo_tts_amd import distributed as D
+    from echo_tts_amd import ops
+    from echo_tts_amd import synthetic as SY
+    from echo_tts_amd import weights as W
+    from echo_tts_amd.model import EchoDiTHip
+    m = EchoDiTHip(E.FULL, W.fast_random_state_dict(E.FULL, "cuda:0", torch.bfloat16, seed=1234), device="cuda:0",
+                   dtype=torch.bfloat16)
+    ids, tm = SY.text_inputs(world)
+    spk, sm = SY.speaker_inputs(world)
+    args = tuple(t.to("cuda:0") for t in (spk, sm, ids, tm))
+    if policy:
+        lat = D.sample_euler_cfg_sharded(m, *args, 11, sequence_length=640, **FULL_KW).cpu()
+    else:  # the round-3 behaviour: splits chosen from the rank's own rows
+        with ops.policy_rows(1, 1):
+            s, e = D.shard_range(world, world, rank)
+            from echo_tts_amd.inference import sample_with_noise
+            noise = torch.randn((world, 640, 80), device="cuda:0", generator=torch.Generator("cuda:0").manual_seed(11))
+            own = sample_with_noise(m, *(t[s:e] for t in args), noise[s:e], **FULL_KW)
+            lat = D.gather_rows(own, world).cpu()
+    q.put((rank, lat.numpy()))
+    dist.destroy_process_group()
+
+
+def test_one_prompt_per_rank_bitwise_equals_one_process():
+    """with one prompt per rank the launches are under-filled and the split choices (GEMM split-K,
+    attention split-KV) of a 1-prompt launch differ from the 2-prompt one-process launch; the sharded sampler
+    takes them for the one-process rows (ops.policy_rows), so the gathered batch is bitwise the one-process
+    result. The same run with per-rank choices differs (it is fp32-close), which shows the test can fail."""
+    import echo_tts_amd as E
+    from echo_tts_amd import synthetic as SY
+    from echo_tts_amd import weights as W
+    from echo_tts_amd.inference import sample_with_noise
+    from echo_tts_amd.model import EchoDiTHip
+    world = 2
+    res = {}
+    for policy in (True, False):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_full_worker, args=(r, world, port, q, policy)) for r in range(world)]
+        for p in procs:
+            p.start()
+        got = {}
+        for _ in range(world):
+            r, lat = q.get(timeout=200)
+            got[r] = torch.from_numpy(lat)
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        assert torch.equal(got[0], got[1])
+        res[policy] = got[0]
+    m = EchoDiTHip(E.FULL, W.fast_random_state_dict(E.FULL, "cuda:0", torch.bfloat16, seed=1234), device="cuda:0",
+                   dtype=torch.bfloat16)
+    ids, tm = SY.text_inputs(world)
+    spk, sm = SY.speaker_inputs(world)
+    noise = torch.randn((world, 640, 80), device="cuda:0", generator=torch.Generator("cuda:0").manual_seed(11))
+    full = sample_with_noise(m, *(t.to("cuda:0") for t in (spk, sm, ids, tm)), noise, **FULL_KW).cpu()
+    assert torch.isfinite(full).all()
+    assert torch.equal(res[True], full), float((res[True] - full).abs().max())
+    e = float((res[False] - full).norm() / full.norm())
+    print(f"[per-rank split choices] rel-L2 to the one-process run {e:.3e}")
+    assert not torch.equal(res[False], full) and e < 5e-2

@@ -818,6 +818,97 @@ def test_gemm_headnorm_t320(M, H, pos0, rh, K):
         assert torch.equal(got, ref), tile
 
 
+SK_CFGS = (1, 2, 3, 4, 5, 6, 7, 8, 9)
+
+
+def _sk_case(M, N, K, epi, seed=0):
+    from echo_tts_amd.model import rope_table_cpu
+    g = torch.Generator(DEV).manual_seed(seed)
+    a = torch.randn(M, K, device=DEV, generator=g).to(BF)
+    w = (torch.randn(N, K, device=DEV, generator=g) * 0.05).to(BF)
+    nout = N // 2 if epi == L.EPI_SWIGLU else N
+    h = torch.randn(M, nout + 64, device=DEV, generator=g).to(BF)
+    gate = torch.tanh(torch.randn(nout, device=DEV, generator=g)).to(BF)
+    hn = None
+    if epi == L.EPI_HEADNORM:
+        H = N // 512
+        nw = (1 + 0.1 * torch.randn(2, H, 128, device=DEV, generator=g)).to(BF)
+        hn = ops.HeadNorm(nw, H, 2, 1e-5, w_stride=H * 128, rope=rope_table_cpu(128, 4096).to(DEV),
+                          rope_heads=H // 2, seq_len=160 if M % 160 == 0 else M, pos0=7)
+    return a, w, h, gate, hn, nout
+
+
+def _sk_run(a, w, h, gate, hn, nout, epi, tile):
+    buf = h.clone()
+    o = buf[:, :nout]
+    if epi == L.EPI_RESID:
+        ops.gemm(a, w, out=o, epilogue=epi, aux=o, gate=gate, tile=tile)
+    elif epi == L.EPI_HEADNORM:
+        ops.gemm(a, w, out=o, tile=tile, head_norm=hn)
+    else:
+        ops.gemm(a, w, out=o, epilogue=epi, tile=tile)
+    assert torch.equal(buf[:, nout:], h[:, nout:])  # padding columns untouched
+    return buf
+
+
+@pytest.mark.parametrize("M,N,K", [(640, 2048, 2048), (160, 2048, 5888), (200, 1024, 256), (1920, 512, 128)])
+@pytest.mark.parametrize("epi", [L.EPI_STORE, L.EPI_SWIGLU, L.EPI_RESID, L.EPI_HEADNORM])
+def test_gemm_small_m_unsplit_bitwise(M, N, K, epi):
+    """The small-M kernel family (gemm_bf16_sk_kernel, `tile` 1C1) without a K split accumulates every
+    element in the K order all bf16 kernels share: bitwise equal to the 2-phase 256x256 kernel for every
+    config — the fused register epilogue where the wave tile allows it, the finish kernel otherwise (head
+    norm always: bitwise equal to the fused epilogue / store + head_norm_rope). Ragged M, in place on a
+    column slice of a wider buffer."""
+    a, w, h, gate, hn, nout = _sk_case(M, N, K, epi)
+    ref = _sk_run(a, w, h, gate, hn, nout, epi, 13)
+    for c in SK_CFGS:
+        got = _sk_run(a, w, h, gate, hn, nout, epi, 100 + 10 * c + 1)
+        assert torch.equal(got, ref), c
+    with ops.gemm_no_splitk():  # the auto pick without splits: the same order
+        assert torch.equal(_sk_run(a, w, h, gate, hn, nout, epi, 0), ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(640, 2048, 5888), (480, 2048, 2048), (160, 11776, 2048), (333, 1024, 512)])
+@pytest.mark.parametrize("epi", [L.EPI_STORE, L.EPI_SWIGLU, L.EPI_RESID, L.EPI_HEADNORM])
+def test_gemm_small_m_split_k(M, N, K, epi):
+    """K split over S workgroups (fp32 partial slabs summed in order by gemm_splitk_finish_kernel, then the
+    fused epilogue): within the rounding of the unsplit kernel, i.e. close to an fp64 reference — every
+    epilogue, S = 2 .. 8 (uneven K-tile ranges), every config; and deterministic (two runs bitwise equal)."""
+    a, w, h, gate, hn, nout = _sk_case(M, N, K, epi)
+    ref = _sk_run(a, w, h, gate, hn, nout, epi, 13).float().cpu()
+    for c in SK_CFGS:
+        for S in (2, 3, 8):
+            if K // 64 < S:
+                continue
+            got = _sk_run(a, w, h, gate, hn, nout, epi, 100 + 10 * c + S)
+            assert torch.isfinite(got.float()).all()
+            e = rel(got, ref)
+            assert e < 4e-3, (c, S, e)
+            if c == 1 and S == 3:
+                assert torch.equal(got, _sk_run(a, w, h, gate, hn, nout, epi, 100 + 10 * c + S))
+    auto = _sk_run(a, w, h, gate, hn, nout, epi, 0)
+    assert rel(auto, ref) < 4e-3
+    if epi == L.EPI_STORE:
+        close_bf16(auto[:, :nout], rb(ref_linear(a, w)))
+
+
+def test_gemm_small_m_policy_rows():
+    """echo_set_policy_rows: the split decision for a launch of M rows taken as for M * num / den rows —
+    a rank holding 1 of 8 prompts splits K exactly like the one-process run of 8 prompts (here: not at
+    all), so its rows are bitwise those of that run."""
+    M1, N, K = 160, 2048, 5888
+    a8 = torch.randn(8 * M1, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    full = ops.gemm(a8, w)
+    one = ops.gemm(a8[:M1].contiguous(), w)
+    with ops.policy_rows(8, 1):
+        one_p = ops.gemm(a8[:M1].contiguous(), w)
+    assert torch.equal(one_p, full[:M1])
+    assert rel(one, full[:M1]) < 4e-3
+    lib = L.load()
+    assert lib.echo_set_policy_rows(1, 2) != 0 and lib.echo_set_policy_rows(0, 1) != 0
+
+
 def test_gemm_headnorm_rejects_bad_args():
     a = torch.randn(64, 64, device=DEV).to(BF)
     w = torch.randn(512, 64, device=DEV).to(BF)

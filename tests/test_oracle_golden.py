@@ -93,3 +93,21 @@ def test_full_c1_fp32():
     lat = O.sample_euler_cfg(S, cfg, g["speaker_latent"], g["speaker_mask"], g["text_ids"], g["text_mask"],
                              g["noise"], dtype=torch.float32, **meta["kw"])
     assert rel_l2(lat, g["latent"]) < 1e-5
+
+
+def test_trajectory_floor_fixture_consistent():
+    """tests/golden/full_traj_sensitivity (the reference's bf16 C2 / C5 samplers re-run with one x_T element
+    moved by one bf16 ulp, make_golden_traj_sensitivity.py): the recorded distances are the distances of the
+    stored latents to the recorded bf16 runs, and both sites give a floor of the same size (~2.6e-2)."""
+    import json
+    import os
+    from safetensors.torch import load_file
+    from conftest import GOLDEN, rel_l2
+    g = load_file(os.path.join(GOLDEN, "full_traj_sensitivity.safetensors"))
+    meta = json.load(open(os.path.join(GOLDEN, "full_traj_sensitivity.json")))
+    for cfg, ref in (("c2", "full_c2_e2e"), ("c5", "full_c5_blk")):
+        r16 = load_file(os.path.join(GOLDEN, ref + ".safetensors"))["bf16.latent"]
+        for j in (0, 1):
+            d = rel_l2(g[f"{cfg}.pert{j}.latent"], r16)
+            assert abs(d - meta["dist"][f"{cfg}.pert{j}"]) < 1e-9 * max(1.0, d)
+            assert 1e-2 < d < 5e-2

@@ -5,6 +5,8 @@ rule 24), random operands, HIP events on the launch stream. Also checks that eac
 config's output is bitwise equal to config 1 (same K accumulation order).
     python tools/bench_gemm.py [--tiles 1,6] [--rounds 5]
 Tile -8: the auto pick with the column split of 320-row launches off (echo_gemm_set_diag key 8).
+Tile 1CS: the small-M kernel, config C (1..6), K split S (1..9); split outputs differ from the unsplit
+order by fp32 rounding (printed as rel-L2 against the first tile).
 """
 import argparse
 import os
@@ -30,13 +32,14 @@ SHAPES = [  # name, M, N, K, epilogue
 
 
 def gemm_t(a, w, t, **kw):
-    """ops.gemm with tile t; t = -8: auto pick, column split of 320-row launches off"""
-    if t == -8:
-        L.load().echo_gemm_set_diag(8, 1)
+    """ops.gemm with tile t; t = -8: auto pick, column split of 320-row launches off; t = -11: auto pick
+    without K splits; t = -12: the round-3 auto pick (no small-M kernel)"""
+    if t in (-8, -11, -12):
+        L.load().echo_gemm_set_diag(-t, 1)
         try:
             return ops.gemm(a, w, tile=0, **kw)
         finally:
-            L.load().echo_gemm_set_diag(8, 0)
+            L.load().echo_gemm_set_diag(-t, 0)
     return ops.gemm(a, w, tile=t, **kw)
 
 
@@ -56,6 +59,7 @@ def timeit_fill(out, args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", default="1,6")
+    ap.add_argument("--sk", default=None, help="add small-M tiles 1CS for configs C x splits S, e.g. 1-6x1,2,3")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--torch", action="store_true", help="also time torch.nn.functional.linear (hipBLASLt)")
@@ -77,6 +81,10 @@ def main():
             v = [int(x) for x in sp.split(",")]
             shapes.append((f"M{v[0]}", v[0], v[1], v[2], v[3] if len(v) > 3 else L.EPI_STORE))
     tiles = [int(t) for t in args.tiles.split(",")]
+    if args.sk:
+        cs, ss = args.sk.split("x")
+        c0, c1 = (int(v) for v in cs.split("-")) if "-" in cs else (int(cs), int(cs))
+        tiles += [100 + 10 * c + int(sv) for c in range(c0, c1 + 1) for sv in ss.split(",")]
     dev = "cuda"
     torch.manual_seed(0)
     for name, M, N, K, epi in shapes:
@@ -94,6 +102,8 @@ def main():
             outs[t] = o
         base = outs[tiles[0]]
         same = {t: bool(torch.equal(outs[t], base)) for t in tiles}
+        err = {t: float((outs[t].double() - base.double()).norm() / base.double().norm().clamp_min(1e-30))
+               for t in tiles}
         times = {t: [] for t in tiles}
         out = torch.empty(M, nout + args.pad_c, device=dev,
                           dtype=torch.float32 if epi == L.EPI_F32OUT else torch.bfloat16)[:, :nout]
@@ -124,7 +134,7 @@ def main():
         line = f"{name} N={N:5d} K={K:4d} [fill {fill * 1e3:6.1f}us {out.numel() * 2 / fill / 1e9:5.2f}TB/s]:"
         for t in tiles:
             ms = sorted(times[t])[len(times[t]) // 2]
-            line += f"  t{t} {ms * 1e3:7.1f}us {fl / ms / 1e9:6.0f}TF{'' if same[t] else ' MISMATCH'}"
+            line += f"  t{t} {ms * 1e3:7.1f}us {fl / ms / 1e9:6.0f}TF{'' if same[t] else f' (rel {err[t]:.1e})'}"
         if tl is not None:
             line += f"  torch {tl * 1e3:7.1f}us {fl / tl / 1e9:6.0f}TF"
         print(line, flush=True)
