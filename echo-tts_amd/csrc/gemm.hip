@@ -2436,26 +2436,6 @@ int64_t sk_ws_bytes(const EchoGemmArgs* a, int c, int S) {
   return sk_partial(c, S, ek_of(a)) ? (int64_t)S * a->M * a->N * 4 : 0;
 }
 
-// Cost model of a small-M launch (seconds), calibrated on MI355X (tools/bench_gemm.py --sk sweep,
-// profiles/r4_sk_sweep.txt): each unit pulls (BM + BN) x K/S x 2 B into LDS at ≈ SK_RCU per CU (shared by
-// the co-resident units) or is MFMA-bound at SK_PCU, plus a fixed per-unit cost; a split / partial launch
-// adds the fp32 slabs' round trip and the finish kernel.
-constexpr double SK_RCU = 80e9, SK_PCU = 7.5e12, SK_T0 = 1.5e-6, SK_TFIN = 2.0e-6, SK_BWFIN = 4.0e12;
-double sk_cost(const EchoGemmArgs* a, int c, int S, int64_t M, int cus) {
-  const SkCfg& k = kSk[c];
-  const int64_t tiles = ((M + k.bm - 1) / k.bm) * ((a->N + k.bn - 1) / k.bn);
-  const int occ = sk_occ(c);
-  const double units = (double)tiles * S;
-  const double rounds = ceil(units / ((double)cus * occ));
-  const double kk = (double)a->K / S;
-  const double t_in = (double)(k.bm + k.bn) * kk * 2 * occ / SK_RCU;
-  const double t_mf = 2.0 * k.bm * k.bn * kk * occ / SK_PCU;
-  double t = rounds * (fmax(t_in, t_mf) + SK_T0);
-  if (sk_partial(c, S, ek_of(a)))
-    t += SK_TFIN + (double)S * M * a->N * 4 * 2 / SK_BWFIN;
-  return t;
-}
-
 // the small-M plan: config and K split from the POLICY rows (echo_set_policy_rows: the rows the launch
 // would have in a one-process run of the whole batch), so that the split — the only choice that changes
 // the summation order — is the one-process choice on every rank
@@ -2464,22 +2444,22 @@ int64_t policy_rows(int64_t rows) { return rows * g_policy_num / g_policy_den; }
 bool sk_plan(const EchoGemmArgs* a, bool allow_split, int* cfg, int* split) {
   if (g_gemm_no_sk || !sk_ok(a)) return false;
   const int64_t Mp = policy_rows(a->M);
-  // only launches the large tiles leave under-filled (pick_tile takes a small config there)
-  if (pick_tile((int)std::min<int64_t>(Mp, 1 << 30), a->N, a->K, 1) == 1) return false;
-  const int cus = cu_count_cached();
-  const int nk = a->K / BK;
-  double best = 1e300;
-  int bc = 0, bs = 1;
-  for (int c = 1; c <= kNumSk; ++c) {
-    for (int S = 1; S <= 8; ++S) {
-      if (S > 1 && (!allow_split || g_gemm_no_splitk || nk < 2 * S)) break;
-      const double e = sk_cost(a, c, S, Mp, cus);
-      if (e < best * 0.999) { best = e; bc = c; bs = S; }
-    }
-  }
-  *cfg = bc;
-  *split = bs;
-  return bc > 0;
+  // Measured (profiles/r4_sk_sweep.txt: every config x split against the round-3 pick and hipBLASLt, MI355X,
+  // interleaved): the small-M family wins only on the gated-residual shapes of the B = 1 / blockwise decoder
+  // (N = 2048) at up to 768 rows, where the round-3 tiles leave most CUs idle on a long K (K = 5888:
+  // M = 160 33.6 -> 16.4 us, M = 480 33.5 -> 25.7, M = 640 38.0 -> 29.5; K = 2048: 15.1 -> 11.8, 14.0 ->
+  // 12.8, 16.9 -> 15.6). Elsewhere (QKVG / W13, M = 1920) the round-3 picks are as fast or faster.
+  if (ek_of(a) != EK_RESID || a->N > 2048 || a->N < 1024 || Mp > 768) return false;
+  const bool longk = a->K >= 4096;
+  int c, S;
+  if (Mp <= 256) { c = 3; S = longk ? 4 : 2; }
+  else if (Mp <= 512) { c = longk ? 3 : 8; S = longk ? 2 : 1; }
+  else { c = longk ? 6 : 3; S = longk ? 3 : 1; }
+  if (!allow_split || g_gemm_no_splitk) S = 1;
+  S = std::max(1, std::min(S, a->K / BK / 2));
+  *cfg = c;
+  *split = S;
+  return true;
 }
 
 }  // namespace
