@@ -721,14 +721,26 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
 // ABL (timing ablations, variants 12-19; results wrong except 32): 1 no loop DMA, 2 no X body, 4 no Y body,
 // 8 no end-of-tile wait + barrier, 16 no tile loop; 32 (diagnostic, results right): CFG rows of one prompt
 // (r, r + B, r + 2B; B = segment 1's batch_mod) adjacent in the block order; 64 (diagnostic, results right):
-// longest-first block order per XCD; 128 (results right): V(t+1)'s DMA between the X and Y bodies
+// longest-first block order per XCD; 128 (results right): V(t+1)'s DMA between the X and Y bodies (NK = NV = 2)
 // NW: waves per workgroup (4: 128 queries, two workgroups per CU; 8: 256 queries, one workgroup per CU, each
 // K/V tile staged once for twice the queries)
-template <int ABL, int NW = 4>
-__global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgpu_num_vgpr(96)))
+// NK / NV: K / V tiles in the LDS ring (16 KiB each). K(j) lives in slot j % NK, V(j) in slot j % NV. At the
+// top of tile t the slots of K(t) and V(t - 1) are free (read before the previous barrier) and take K(t + NK)
+// and V(t + NV - 1); the end-of-tile wait needs only K(t + 2) and V(t + 1) (read in tile t + 1), so with
+// NK, NV >= 3 the DMA issued in tile t stays in flight across the barrier (a counted vmcnt: V is issued first,
+// K second, both younger than every piece the wait needs) and each tile's loads get two tiles of latency
+// budget instead of one (NK = NV = 2 waits vmcnt(0) for the loads it issued at its own top). LDS: (NK + NV) x
+// 16 KiB — 2 + 2 and 3 + 2 keep two workgroups per CU, 3 + 3 and 4 + 4 one.
+template <int ABL, int NW = 4, int NK = 2, int NV = 2>
+__global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __attribute__((amdgpu_num_vgpr(96)))
     attn_pl_kernel(EchoAttnArgs a_arg) {
   constexpr int QB = 32 * NW, DPT = 16 / NW, KTT = KT;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[4 * KT * 128];  // K slot 0, 1 | V slot 0, 1
+  static_assert(NK >= 2 && NV >= 2 && NK <= 4 && NV <= 4, "ring slots (attn_pl.inc MAX_SLOTS)");
+  static_assert(!(ABL & 128) || (NK == 2 && NV == 2), "ablation 128 is defined on the 2 + 2 ring");
+  // unroll period lcm(2, NK, NV): slots and score buffers are literals of the bodies (3 with 4 would need 12)
+  constexpr int PER = (NK == 3 || NV == 3) ? 6 : (NK == 4 || NV == 4) ? 4 : 2;
+  static_assert(PER % NK == 0 && PER % NV == 0, "unsupported ring combination");
+  __shared__ __attribute__((aligned(16))) bf16_t lds[(NK + NV) * KT * 128];  // K slots | V slots
 
   using KArgs = const __attribute__((address_space(4))) EchoAttnArgs;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -767,11 +779,12 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
 
   ECHO_SEG_TABLE()
   ECHO_CURSOR_ADVANCE()
-  Cursor kc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // K DMA (two tiles ahead of PV)
-  Cursor vc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // V DMA (one tile ahead)
+  Cursor kc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // K DMA (NK - 1 tiles ahead of the QK)
+  Cursor vc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // V DMA (NV - 1 tiles ahead of the PV)
   Cursor mc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // the tile whose scores are masked / maxed
 
   const int dr = lane >> 4, dp = lane & 15;
+  // one tile's share of this wave (DPT pieces) into slot `slot` of the K (part 0) or V (part 1) ring
   auto dma_part = [&](Cursor& c, int part, int slot) __attribute__((always_inline)) {
     advance(c);
     const int last = c.kend - 1 - c.t0;
@@ -781,7 +794,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
       const int r = (i * NW + w) * 4 + dr;
       const uint32_t voff = (uint32_t)(min(r, last) * c.ld + ((dp ^ swz(r)) * 8)) * 2u;
       const uint32_t dst = __builtin_amdgcn_readfirstlane(
-          lds_addr_of(lds + (part * 2 + slot) * KT * 128 + ((i * NW + w) * 4) * 128));
+          lds_addr_of(lds + (part * NK + slot) * KT * 128 + ((i * NW + w) * 4) * 128));
       glds16s(base, voff, dst);
     }
   };
@@ -798,8 +811,8 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       const int ch = 4 * dt + 2 * (g & 1) + (p4 >> 1);
-      va[2 * dt] = lbase + 2u * KT * 128 * 2 + (uint32_t)(r0 * 128 + ((ch ^ swz(r0)) * 8) + (p4 & 1) * 4) * 2u;
-      va[2 * dt + 1] = lbase + 2u * KT * 128 * 2 + (uint32_t)(r1 * 128 + ((ch ^ swz(r1)) * 8) + (p4 & 1) * 4) * 2u;
+      va[2 * dt] = lbase + (uint32_t)NK * KT * 128 * 2 + (uint32_t)(r0 * 128 + ((ch ^ swz(r0)) * 8) + (p4 & 1) * 4) * 2u;
+      va[2 * dt + 1] = lbase + (uint32_t)NK * KT * 128 * 2 + (uint32_t)(r1 * 128 + ((ch ^ swz(r1)) * 8) + (p4 & 1) * 4) * 2u;
     }
   }
 
@@ -833,16 +846,31 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
   };
 
   pl_zero_o();
-  // prologue: K(0), V(0), K(1); scores, mask and max of tile 0
+  // prologue: K(0), V(0), K(1) — needed before tile 0's loop iteration — then V(1 .. NV-2), K(2 .. NK-1), which
+  // may stay in flight; scores, mask and max of tile 0
   if (ntiles > 0) { dma_part(kc, 0, 0); dma_part(vc, 1, 0); }
   if (ntiles > 1) dma_part(kc, 0, 1);
+#pragma unroll
+  for (int j = 1; j <= NV - 2; ++j)
+    if (j < ntiles) dma_part(vc, 1, j);
+#pragma unroll
+  for (int j = 2; j <= NK - 1; ++j)
+    if (j < ntiles) dma_part(kc, 0, j);
   // Q and the prologue DMA in flight together: one wait (hipcc's vmcnt(0) for Q covers the DMA issued after it)
 #pragma unroll
   for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  {
+    const int younger = (min(NV - 1, ntiles) - 1 > 0 ? min(NV - 1, ntiles) - 1 : 0) +
+                        (min(NK, ntiles) - 2 > 0 ? min(NK, ntiles) - 2 : 0);  // pieces issued after K(1)
+    if (NK + NV == 4 || younger == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(DPT) : "memory");
+    else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * DPT) : "memory");
+    else if (younger == 3) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(3 * DPT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(4 * DPT) : "memory");
+  }
   if (ntiles > 0) {
     if (wact) {
-      pl_qk_0(qf, ka);
+      pl_qk_cs<0, 0>(qf, ka);
       mask_tile(std::integral_constant<int, 0>{});
       float mx, ma;
       pl_max_0(mx, ma);
@@ -851,13 +879,22 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
       advance(mc);
     }
   }
-  asm volatile("s_barrier" ::: "memory");  // every wave's K(0) reads are done: slot 0 takes K(2)
+  asm volatile("s_barrier" ::: "memory");  // every wave's K(0) reads are done: slot 0 takes K(NK)
 
-  auto iter = [&](int t, auto par) __attribute__((always_inline)) {
-    constexpr int P = decltype(par)::value;
-    if (t + 2 < ntiles && !(ABL & 1)) dma_part(kc, 0, P);      // K(t+2) -> K slot t & 1 (K(t) was read in X(t-1))
-    // V(t+1) -> V slot (t+1) & 1 (V(t-1) was read in Y(t-1)); ABL 128: issued between X(t) and Y(t) instead
-    if (!(ABL & 128) && t + 1 < ntiles && !(ABL & 1)) dma_part(vc, 1, 1 - P);
+  auto iter = [&](int t, auto unr) __attribute__((always_inline)) {
+    constexpr int U = decltype(unr)::value;  // t mod PER
+    constexpr int P = U & 1;                 // score buffer of tile t
+    constexpr int KS = (U + 1) % NK;         // K slot of tile t + 1 (its QK runs in X(t))
+    constexpr int VS = U % NV;               // V slot of tile t (its PV runs in Y(t))
+    int issued = 0;                          // DMA tiles of this wave issued at this tile's top
+    if constexpr (NK == 2 && NV == 2) {
+      if (t + 2 < ntiles && !(ABL & 1)) dma_part(kc, 0, P);      // K(t+2) -> K slot t & 1 (K(t) was read in X(t-1))
+      // V(t+1) -> V slot (t+1) & 1 (V(t-1) was read in Y(t-1)); ABL 128: issued between X(t) and Y(t) instead
+      if (!(ABL & 128) && t + 1 < ntiles && !(ABL & 1)) dma_part(vc, 1, 1 - P);
+    } else {
+      if (t + NV - 1 < ntiles && !(ABL & 1)) { dma_part(vc, 1, (U + NV - 1) % NV); ++issued; }  // V first
+      if (t + NK < ntiles && !(ABL & 1)) { dma_part(kc, 0, U % NK); ++issued; }
+    }
     const float msc = m_run == -INFINITY ? 0.f : -m_run * sl2;
     float ps;
     if (!wact) {
@@ -865,25 +902,45 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
       if ((ABL & 128) && !(ABL & 1) && t + 1 < ntiles) dma_part(vc, 1, 1 - P);
     } else if (t + 1 < ntiles) {
       ps = 0.f;
-      if constexpr (!(ABL & 2)) { if constexpr (P == 0) pl_x_0(qf, ka, sl2, msc, ps); else pl_x_1(qf, ka, sl2, msc, ps); }
+      if constexpr (!(ABL & 2)) pl_x_cs<P, KS>(qf, ka, sl2, msc, ps);
       l_run += ps;
       mask_tile(std::integral_constant<int, 1 - P>{});
       if ((ABL & 128) && !(ABL & 1)) dma_part(vc, 1, 1 - P);
       float mx = 0.f, ma;
-      if constexpr (!(ABL & 4)) { if constexpr (P == 0) pl_y_0(va, mx, ma); else pl_y_1(va, mx, ma); }
+      if constexpr (!(ABL & 4)) pl_y_cs<P, VS>(va, mx, ma);
       decide(mx);
     } else {
       if constexpr (P == 0) pl_xl_0(sl2, msc, ps); else pl_xl_1(sl2, msc, ps);
       l_run += ps;
-      if constexpr (P == 0) pl_yl_0(va); else pl_yl_1(va);
+      pl_yl_cs<P, VS>(va);
     }
-    if constexpr (!(ABL & 8)) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (!(ABL & 8)) {
+      // K(t+2) and V(t+1) must have landed (every wave's share, then the barrier); with NK, NV >= 3 the tiles
+      // issued at this tile's top are younger than both and stay in flight (NV == 2: V(t+1) is this tile's V
+      // issue, so only the K issued after it may stay; NK == 2: K(t+2) is this tile's K issue, the youngest)
+      const int keep = (NK == 2 && NV == 2) ? 0 : NK == 2 ? 0 : NV == 2 ? (issued == 2 ? 1 : 0) : issued;
+      if (keep == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      else if (keep == 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(DPT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * DPT) : "memory");
+    }
   };
   if (ABL & 16) ntiles = 0;
-  for (int t = 0; t < ntiles; t += 2) {
+  for (int t = 0; t < ntiles; t += PER) {
     iter(t, std::integral_constant<int, 0>{});
     if (t + 1 >= ntiles) break;
     iter(t + 1, std::integral_constant<int, 1>{});
+    if constexpr (PER >= 4) {
+      if (t + 2 >= ntiles) break;
+      iter(t + 2, std::integral_constant<int, 2 % PER>{});
+      if (t + 3 >= ntiles) break;
+      iter(t + 3, std::integral_constant<int, 3 % PER>{});
+    }
+    if constexpr (PER == 6) {
+      if (t + 4 >= ntiles) break;
+      iter(t + 4, std::integral_constant<int, 4 % PER>{});
+      if (t + 5 >= ntiles) break;
+      iter(t + 5, std::integral_constant<int, 5 % PER>{});
+    }
   }
 
   // ---- epilogue (attn_bf16_kernel's row layout): normalise, round, transpose through LDS, gate, store
@@ -1412,6 +1469,11 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 25: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<128>, grid, dim3(256), 0, s, *a); break;
     case 23: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<64>, grid, dim3(256), 0, s, *a); break;
     case 24: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<32>, grid, dim3(256), 0, s, *a); break;
+    // asm pipeline with deeper K / V rings (NK + NV slots of 16 KiB; counted waits keep each tile's DMA in
+    // flight across its barrier): 26 = 3 + 2 (80 KiB, two workgroups per CU), 27 = 3 + 3, 28 = 4 + 4 (one per CU)
+    case 26: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 3, 2>), grid, dim3(256), 0, s, *a); break;
+    case 27: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 3, 3>), grid, dim3(256), 0, s, *a); break;
+    case 28: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 4, 4>), grid, dim3(256), 0, s, *a); break;
     case 20: case 21: case 22: {  // asm pipeline at 8 waves x 32 queries (21: no tile loop, 22: no X / Y bodies)
       if (any_causal(a)) return ECHO_EINVAL;
       const dim3 g8(attn_grid(a, 256));

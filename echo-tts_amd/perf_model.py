@@ -126,9 +126,10 @@ class GemmTimer:
             return {"launches": 0}
         avg_ms = sum(ms) / n
         avg_fl = sum(fl) / n
-        return {"launches": n, "avg_ms": avg_ms, "avg_flop": avg_fl,
-                "avg_bytes": sum(r[5] for r in self.records) / n,
-                "tflops": avg_fl / (avg_ms * 1e-3) / 1e12}
+        avg_b = sum(r[5] for r in self.records) / n
+        return {"launches": n, "avg_ms": avg_ms, "avg_flop": avg_fl, "avg_bytes": avg_b,
+                "tflops": avg_fl / (avg_ms * 1e-3) / 1e12, "gbs": avg_b / (avg_ms * 1e-3) / 1e9,
+                "total_ms": avg_ms * n}
 
 
 class AttnTimer:

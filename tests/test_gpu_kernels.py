@@ -542,6 +542,13 @@ def test_attention_pipeline_bitwise(case):
         got.fill_(float("nan"))
         ops.attention(q[:, :, 0], segs, out=got, gate=gate)
     assert torch.equal(got, ref)
+    # deeper K / V rings (variants 26 / 27 / 28: 3 + 2, 3 + 3, 4 + 4 slots, counted waits across the barrier):
+    # the same bodies on other LDS slots, bitwise equal
+    for v in (26, 27, 28):
+        got.fill_(float("nan"))
+        ops.attention_variant(q[:, :, 0], segs, out=got, gate=gate, variant=v)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref), (v, float((got != ref).double().mean()))
     if case in ("one_tile", "one_query", "spikes"):
         close_bf16(ref, ref_attention(q[:, :, 0], segs, gate, 128 ** -0.5, BF))
 

@@ -11,6 +11,10 @@ attn_pl_kernel (attention.hip) caps the compiler at 96 VGPRs (amdgpu_num_vgpr) a
     v224 .. v239   K fragment ring, 4 slots of 4 registers
     v240 .. v255   V^T fragment ring, 4 slots of 4 registers (2 transposed b64 reads each)
 
+The LDS ring slot of the K / V tile a body reads is a literal of the body (pl_x_<buffer>_<K slot>,
+pl_y_<buffer>_<V slot>, up to MAX_SLOTS slots of 16 KiB each; pl_x_cs<C, S> etc. dispatch at compile time),
+so attn_pl_kernel<.., NK, NV> can keep NK K tiles and NV V tiles in its LDS ring.
+
 Each function below is ONE asm statement over those registers, so the compiler never sees (and never
 copies, splits or spills) the loop state; it keeps only addresses, Q and the softmax scalars. The math and
 its order are attn_bf16_kernel<0, 4, 2>'s, instruction for instruction (bitwise-equal results):
@@ -208,46 +212,54 @@ KIN = [f"[ka{d}] \"v\"(ka[{d}])" for d in range(8)]
 VIN = [f"[va{d}] \"v\"(va[{d}])" for d in range(8)]
 
 
+MAX_SLOTS = 4  # K / V ring slots addressable by the bodies (immediate LDS offsets stay < 64 KiB)
+
+
 def gen():
     fns = []
     for par in (0, 1):
-        # the score buffer of tile t is buffer t & 1; K(t+1) sits in K slot (t+1) & 1, V(t) in V slot t & 1
+        # the score buffer of tile t is buffer t & 1; with NK K slots and NV V slots (attn_pl_kernel<.., NK, NV>)
+        # K(j) sits in K slot j % NK and V(j) in V slot j % NV: the bodies take the slot as a literal
         c, n = par, 1 - par
-        # QK only (tile 0 of an item: buffer 0, K slot 0; generic over parity for completeness)
-        fns.append(asm_fn(f"pl_qk_{par}(const bf16x8 (&q)[8], const uint32_t (&ka)[8])",
-                          [t for _, t in qk_stream(par, par)], [], QIN + KIN,
-                          comment=f"scores of a tile whose K is in slot {par} into buffer {par}"))
-        # X: softmax(t) || QK(t+1)
-        body = interleave(qk_stream(n, n), softmax_stream(c), lead=8)
-        fns.append(asm_fn(f"pl_x_{par}(const bf16x8 (&q)[8], const uint32_t (&ka)[8], float sl2, float msc, float& ps)",
-                          body, ['[ps] "=&v"(ps)'], QIN + KIN + ['[sl2] "v"(sl2)', '[msc] "v"(msc)'],
-                          comment=f"tile t (t & 1 = {par}): softmax of buffer {c} || QK of tile t+1 into buffer {n}"))
+        for ks in range(MAX_SLOTS):
+            # QK only (tile 0 of an item: buffer 0, K slot 0)
+            fns.append(asm_fn(f"pl_qk_{par}_{ks}(const bf16x8 (&q)[8], const uint32_t (&ka)[8])",
+                              [t for _, t in qk_stream(par, ks)], [], QIN + KIN,
+                              comment=f"scores of a tile whose K is in slot {ks} into buffer {par}"))
+            # X: softmax(t) || QK(t+1)
+            body = interleave(qk_stream(n, ks), softmax_stream(c), lead=8)
+            fns.append(asm_fn(f"pl_x_{par}_{ks}(const bf16x8 (&q)[8], const uint32_t (&ka)[8], float sl2, float msc, "
+                              f"float& ps)",
+                              body, ['[ps] "=&v"(ps)'], QIN + KIN + ['[sl2] "v"(sl2)', '[msc] "v"(msc)'],
+                              comment=f"tile t (t & 1 = {par}): softmax of buffer {c} || QK of tile t+1 (K slot {ks}) "
+                                      f"into buffer {n}"))
         fns.append(asm_fn(f"pl_xl_{par}(float sl2, float msc, float& ps)",
                           softmax_stream(c), ['[ps] "=&v"(ps)'], ['[sl2] "v"(sl2)', '[msc] "v"(msc)'],
                           comment=f"last tile (t & 1 = {par}): softmax of buffer {c} only"))
-        # Y: PV(t) || max(t+1)
-        pv = pv_stream(c, c)
-        mx = max_stream(n)
-        # the max goes into the gaps after PV MFMA 4 .. 15 (its NOP20 keeps the QK results of X safe to read)
-        res, m = [], 0
-        mi = 0
-        for line in interleave(pv, [], 0):
-            res.append(line)
-            if line.startswith("v_mfma"):
-                m += 1
-                if m >= 4:
-                    take = (len(mx) - mi) // (16 - m + 1) if m < 16 else len(mx) - mi
-                    take = max(take, 0)
-                    res += mx[mi:mi + take]
-                    mi += take
-        res += mx[mi:]
-        res.append("s_waitcnt lgkmcnt(0)")
-        fns.append(asm_fn(f"pl_y_{par}(const uint32_t (&va)[8], float& mx, float& ma)",
-                          res, ['[mx] "=&v"(mx)', '[ma] "=&v"(ma)'], VIN,
-                          comment=f"tile t (t & 1 = {par}): PV from buffer {c}, V slot {c} || row max of buffer {n}"))
-        body = [t for _, t in pv] + ["s_waitcnt lgkmcnt(0)"]
-        fns.append(asm_fn(f"pl_yl_{par}(const uint32_t (&va)[8])", body, [], VIN,
-                          comment=f"last tile (t & 1 = {par}): PV from buffer {c}, V slot {c}"))
+        for vs in range(MAX_SLOTS):
+            # Y: PV(t) || max(t+1)
+            pv = pv_stream(c, vs)
+            mx = max_stream(n)
+            # the max goes into the gaps after PV MFMA 4 .. 15 (its NOP20 keeps the QK results of X safe to read)
+            res, m = [], 0
+            mi = 0
+            for line in interleave(pv, [], 0):
+                res.append(line)
+                if line.startswith("v_mfma"):
+                    m += 1
+                    if m >= 4:
+                        take = (len(mx) - mi) // (16 - m + 1) if m < 16 else len(mx) - mi
+                        take = max(take, 0)
+                        res += mx[mi:mi + take]
+                        mi += take
+            res += mx[mi:]
+            res.append("s_waitcnt lgkmcnt(0)")
+            fns.append(asm_fn(f"pl_y_{par}_{vs}(const uint32_t (&va)[8], float& mx, float& ma)",
+                              res, ['[mx] "=&v"(mx)', '[ma] "=&v"(ma)'], VIN,
+                              comment=f"tile t (t & 1 = {par}): PV from buffer {c}, V slot {vs} || row max of buffer {n}"))
+            body = [t for _, t in pv] + ["s_waitcnt lgkmcnt(0)"]
+            fns.append(asm_fn(f"pl_yl_{par}_{vs}(const uint32_t (&va)[8])", body, [], VIN,
+                              comment=f"last tile (t & 1 = {par}): PV from buffer {c}, V slot {vs}"))
         # max only (tile 0 prologue) of buffer par
         fns.append(asm_fn(f"pl_max_{par}(float& mx, float& ma)", max_stream(par),
                           ['[mx] "=&v"(mx)', '[ma] "=&v"(ma)'], [],
@@ -274,6 +286,22 @@ def gen():
         outs = [f'[o{r}] "=v"(o[{r}])' for r in range(16)]
         fns.append(asm_fn(f"pl_get_o_{dt}(float (&o)[16])", body, outs, [],
                           comment=f"copy o[{dt}] out of the owned registers"))
+    # compile-time dispatch over (buffer parity, slot)
+    disp = []
+    for name, args, call in (
+            ("pl_qk", "const bf16x8 (&q)[8], const uint32_t (&ka)[8]", "q, ka"),
+            ("pl_x", "const bf16x8 (&q)[8], const uint32_t (&ka)[8], float sl2, float msc, float& ps",
+             "q, ka, sl2, msc, ps"),
+            ("pl_y", "const uint32_t (&va)[8], float& mx, float& ma", "va, mx, ma"),
+            ("pl_yl", "const uint32_t (&va)[8]", "va")):
+        lines = [f"template <int C, int S>\n__device__ __forceinline__ void {name}_cs({args}) {{"]
+        for par in (0, 1):
+            for sl in range(MAX_SLOTS):
+                kw = "if" if (par, sl) == (0, 0) else "else if"
+                lines.append(f"  {kw} constexpr (C == {par} && S == {sl}) {name}_{par}_{sl}({call});")
+        lines.append("}")
+        disp.append("\n".join(lines))
+    fns += disp
     hdr = ("// GENERATED by tools/gen_attn_pl.py — do not edit. Hand-scheduled tile bodies of attn_pl_kernel\n"
            "// (attention.hip); register map and bitwise contract in the generator's docstring.\n")
     return hdr + "\n\n".join(fns) + "\n"
