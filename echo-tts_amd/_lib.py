@@ -37,7 +37,8 @@ class GemmArgs(C.Structure):
                 ("hn_w", vp), ("hn_w_stride", i64), ("hn_rope", vp),
                 ("hn_heads", i32), ("hn_nblk", i32), ("hn_rope_heads", i32), ("hn_seq_len", i32),
                 ("hn_pos0", i32), ("hn_pos_mult", i32), ("hn_eps", f32),
-                ("act_alpha", vp), ("conv_c", i32), ("conv_taps", i32), ("conv_dil", i32)]
+                ("act_alpha", vp), ("conv_c", i32), ("conv_taps", i32), ("conv_dil", i32),
+                ("mod_out", vp), ("ld_mod", i64), ("mod_shift", vp), ("mod_scale1", vp), ("mod_eps", f32)]
 
 
 class KVSegment(C.Structure):
@@ -106,7 +107,7 @@ SIGNATURES = {
     "echo_abi_struct_size": (i64, [i32]),
 }
 
-ABI_VERSION = 4  # include/echo_hip.h ECHO_ABI_VERSION
+ABI_VERSION = 5  # include/echo_hip.h ECHO_ABI_VERSION
 # ctypes mirrors of the argument structs, by echo_abi_struct_size id
 ABI_STRUCTS = {0: "GemmArgs", 1: "AttnArgs", 2: "KVSegment", 3: "StepArgs", 4: "RvqWeights"}
 

@@ -39,6 +39,8 @@ struct Epi {
                 // persistent kernel: group-M height (set by launch_ps_ek)
   const void* act_alpha;        // ECHO_ACT_SNAKE
   int conv_c, conv_taps, conv_dil;  // causal-conv A addressing (echo_hip.h)
+  // RESID + the next AdaLN (EchoGemmArgs.mod_*; the split-K finish kernel only)
+  void* mod_out; int64_t ld_mod; const void* mod_shift; const void* mod_scale1; float mod_eps;
 };
 
 // Element offset added to A for the K-slice starting at k0 in conv mode (0 otherwise): tap
@@ -629,10 +631,16 @@ gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __r
 // launch, with the roundings of gemm_epilogue: one thread per 8 output columns of one row (16 B out);
 // EK_HEADNORM: the 16 threads of a (row, 128-column head) are one 16-lane row of the wave (N % 128 == 0),
 // so the sum of squares is the xor-butterfly of head_norm_rope_kernel / the fused epilogue.
-template <int EK>
+// MOD (EK_RESID, N == 2048: the workgroup is one row, thread t = columns 8t .. 8t+7): the updated row is
+// also normalised and modulated into ep.mod_out with adaln_rows_kernel<4>'s arithmetic — there lane l of
+// the row's wave holds the chunks t = c*64 + l (c = 0..3), i.e. the same lane of each of our 4 waves; the
+// rounded row goes through LDS so that every lane sums its 32 squares in that kernel's order before the
+// same wave butterfly, and r, the products and the rounding are the same expressions (bitwise equal).
+template <int EK, bool MOD = false>
 __global__ void __launch_bounds__(256)
 gemm_splitk_finish_kernel(const float* __restrict__ ws, int S, int M, int N, void* __restrict__ Cv, int64_t ldc,
                           Epi ep) {
+  static_assert(!MOD || EK == EK_RESID, "the fused AdaLN follows the residual epilogue");
   const int Nout = EK == EK_SWIGLU ? N / 2 : N;
   const int cpr = Nout / 8;  // 8-column chunks per output row
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -676,6 +684,34 @@ gemm_splitk_finish_kernel(const float* __restrict__ ws, int S, int M, int N, voi
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = x[e] + v[e];  // store8 rounds
+    if constexpr (MOD) {
+      __shared__ float row[2048];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = rbf(v[e]);
+        row[n + e] = v[e];
+      }
+      store8(out, v);
+      __syncthreads();
+      const int lane = threadIdx.x & 63;
+      float ss = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float u = row[(q * 64 + lane) * 8 + e];
+          ss += u * u;
+        }
+      ss = wave_sum(ss);
+      const float r = 1.0f / sqrtf(ss / 2048.0f + ep.mod_eps);
+      float s1[8], sh[8], o[8];
+      load8((const bf16_t*)ep.mod_scale1 + n, s1);
+      load8((const bf16_t*)ep.mod_shift + n, sh);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = ((v[e] * r) * s1[e]) + sh[e];
+      store8((bf16_t*)ep.mod_out + (int64_t)m * ep.ld_mod + n, o);
+      return;
+    }
   } else if constexpr (EK == EK_HEADNORM) {
     const int hidx = n >> 7, ch = (n >> 3) & 15;
     const int blk = hidx / ep.hn_heads, h = hidx - blk * ep.hn_heads;
@@ -2483,7 +2519,8 @@ template <int BM, int BN, int WM, int WN, int NS>
 int launch_sk(const EchoGemmArgs* a, const Epi& ep, int S, void* ws, hipStream_t s) {
   const int ek = ek_of(a);
   const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;
-  if (!(S > 1 || ek == EK_HEADNORM || !sk_direct(BM / WM, BN / WN, ek))) {
+  const bool mod = ep.mod_out != nullptr;  // caller checked: RESID, N == 2048, partial plan
+  if (!mod && !(S > 1 || ek == EK_HEADNORM || !sk_direct(BM / WM, BN / WN, ek))) {
     switch (ek) {
       case EK_STORE: return launch_sk_direct<BM, BN, WM, WN, NS, EK_STORE>(a, ep, s);
       case EK_SWIGLU: return launch_sk_direct<BM, BN, WM, WN, NS, EK_SWIGLU>(a, ep, s);
@@ -2502,7 +2539,10 @@ int launch_sk(const EchoGemmArgs* a, const Epi& ep, int S, void* ws, hipStream_t
   switch (ek) {
     case EK_STORE: hipLaunchKernelGGL(gemm_splitk_finish_kernel<EK_STORE>, g, dim3(256), 0, s, w, S, a->M, a->N, a->C, a->ldc, ep); break;
     case EK_SWIGLU: hipLaunchKernelGGL(gemm_splitk_finish_kernel<EK_SWIGLU>, g, dim3(256), 0, s, w, S, a->M, a->N, a->C, a->ldc, ep); break;
-    case EK_RESID: hipLaunchKernelGGL(gemm_splitk_finish_kernel<EK_RESID>, g, dim3(256), 0, s, w, S, a->M, a->N, a->C, a->ldc, ep); break;
+    case EK_RESID:
+      if (mod) hipLaunchKernelGGL((gemm_splitk_finish_kernel<EK_RESID, true>), g, dim3(256), 0, s, w, S, a->M, a->N, a->C, a->ldc, ep);
+      else hipLaunchKernelGGL(gemm_splitk_finish_kernel<EK_RESID>, g, dim3(256), 0, s, w, S, a->M, a->N, a->C, a->ldc, ep);
+      break;
     case EK_HEADNORM: hipLaunchKernelGGL(gemm_splitk_finish_kernel<EK_HEADNORM>, g, dim3(256), 0, s, w, S, a->M, a->N, a->C, a->ldc, ep); break;
     default: return ECHO_EINVAL;
   }
@@ -2598,7 +2638,40 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
   Epi ep{a->bias, a->stride_bias, a->aux, a->ld_aux, a->stride_aux, a->gate, a->stride_gate,
          a->epilogue, a->act, a->out_div,
          a->hn_w, a->hn_w_stride, a->hn_rope, a->hn_heads, a->hn_nblk, a->hn_rope_heads, a->hn_seq_len,
-         a->hn_pos0, a->hn_pos_mult, a->hn_eps, 0, a->act_alpha, a->conv_c, a->conv_taps, a->conv_dil};
+         a->hn_pos0, a->hn_pos_mult, a->hn_eps, 0, a->act_alpha, a->conv_c, a->conv_taps, a->conv_dil,
+         nullptr, 0, nullptr, nullptr, 0.f};
+  if (a->mod_out) {
+    // residual + the next AdaLN: fused into the finish kernel when the small-M plan has one (K split or
+    // no direct epilogue) and a row is one finish workgroup (N == 2048); else the GEMM, then
+    // echo_adaln_modulate on the rows it wrote (the same kernel arithmetic: bitwise equal)
+    if (a->epilogue != ECHO_EPI_RESID || a->dtype != ECHO_BF16 || a->batch != 1 || !a->mod_shift ||
+        !a->mod_scale1 || a->ldc != a->N || a->ld_mod != a->N || (a->N != 1024 && a->N != 2048 && a->N != 4096) ||
+        ((uintptr_t)a->mod_out | (uintptr_t)a->mod_shift | (uintptr_t)a->mod_scale1) & 15)
+      return ECHO_EINVAL;
+    int c = 0, S = 1;
+    if (a->tile >= 110 && a->tile <= 199) {
+      c = (a->tile / 10) % 10;
+      S = a->tile % 10;
+    } else if (a->tile != 0 || !sk_plan(a, ws != nullptr, &c, &S)) {
+      c = 0;
+    }
+    const int64_t need = c >= 1 && c <= kNumSk && sk_ok(a) ? sk_ws_bytes(a, c, S) : 0;
+    if (a->N == 2048 && need > 0 && a->K / BK >= S && ws && (uintptr_t)ws % 16 == 0 && ws_bytes >= need) {
+      Epi em = ep;
+      em.mod_out = a->mod_out;
+      em.ld_mod = a->ld_mod;
+      em.mod_shift = a->mod_shift;
+      em.mod_scale1 = a->mod_scale1;
+      em.mod_eps = a->mod_eps;
+      return launch_sk_cfg(a, em, c, S, ws, s);
+    }
+    EchoGemmArgs b = *a;
+    b.mod_out = nullptr;
+    const int rc = echo_gemm_ws(&b, ws, ws_bytes, stream);
+    if (rc) return rc;
+    return echo_adaln_modulate(ECHO_BF16, a->C, a->mod_out, a->M, a->N, a->mod_shift, a->mod_scale1, 0, 0,
+                               a->mod_eps, stream);
+  }
   // small-M family (gemm_bf16_sk_kernel): forced (`tile` 1CS) or the auto pick of under-filled launches
   if (a->tile >= 110 && a->tile <= 199) {
     const int c = (a->tile / 10) % 10, S = a->tile % 10;

@@ -11,6 +11,7 @@
 //
 // Reference ops each entry replaces (file:line of /root/reference):
 //   gemm / gemm_out        every nn.Linear + fused tails   model.py:56-62,118-122,177-197,303-308,385-388,602-604
+//   gemm_resid_norm_out    gated residual + next AdaLN     model.py:385,388 + 76-81
 //   joint_attention(_out)  KV concat + SDPA + sigmoid gate model.py:237-264, 144-157; inference.py:409-417
 //   rmsnorm(_out)          RMSNorm                         model.py:99-104
 //   norm_modulate(_out)    LowRankAdaLN normalisation tail model.py:76-83
@@ -115,10 +116,19 @@ GemmSpec gemm_spec(const Tensor& a, const Tensor& w, int64_t epilogue, at::IntAr
   return {A.rows, Wm.rows, K, batch, n_out, epilogue == ECHO_EPI_F32OUT};
 }
 
+// the next AdaLN fused behind a gated residual (gemm_resid_norm_out)
+struct ModArgs {
+  const Tensor& xn;
+  const Tensor& shift;
+  const Tensor& scale1;
+  double eps;
+};
+
 void gemm_launch(const Tensor& a, const Tensor& w, const Tensor& out, const optional<Tensor>& bias,
                  int64_t epilogue, const optional<Tensor>& aux, const optional<Tensor>& gate, int64_t act,
                  double out_div, int64_t tile, const optional<Tensor>& hn_w, const optional<Tensor>& hn_rope,
-                 at::IntArrayRef hn, double hn_eps, const optional<Tensor>& act_alpha, at::IntArrayRef conv) {
+                 at::IntArrayRef hn, double hn_eps, const optional<Tensor>& act_alpha, at::IntArrayRef conv,
+                 const ModArgs* mod = nullptr) {
   need_dev(a, a, "a");
   need_dev(a, w, "w");
   need_dev(a, out, "out");
@@ -208,6 +218,23 @@ void gemm_launch(const Tensor& a, const Tensor& w, const Tensor& out, const opti
     g.hn_pos_mult = i32(hn[6], "hn pos_mult");
     g.hn_eps = (float)hn_eps;
   }
+  if (mod) {
+    need_dev(a, mod->xn, "xn");
+    need_dev(a, mod->shift, "shift");
+    need_dev(a, mod->scale1, "scale1");
+    TORCH_CHECK(epilogue == ECHO_EPI_RESID && s.batch == 1 && out.is_contiguous() && mod->xn.is_contiguous() &&
+                    mod->xn.sizes() == out.sizes() && mod->xn.scalar_type() == a.scalar_type() &&
+                    a.scalar_type() == at::kBFloat16,
+                "echo_hip.gemm_resid_norm: bf16, one batch, contiguous h / xn of equal shape");
+    for (const Tensor* v : {&mod->shift, &mod->scale1})
+      TORCH_CHECK(v->dim() == 1 && v->numel() == s.N && v->is_contiguous() && v->scalar_type() == a.scalar_type(),
+                  "echo_hip.gemm_resid_norm: shift / scale1 must be contiguous [N] of the model dtype");
+    g.mod_out = mod->xn.data_ptr();
+    g.ld_mod = s.N;
+    g.mod_shift = mod->shift.data_ptr();
+    g.mod_scale1 = mod->scale1.data_ptr();
+    g.mod_eps = (float)mod->eps;
+  }
   c10::DeviceGuard guard(a.device());
   // under-filled launches may split K (echo_gemm_ws_bytes > 0): the fp32 partial slabs come from the
   // caching allocator (graph-private pool under hipGraph capture)
@@ -236,6 +263,16 @@ void gemm_out(const Tensor& a, const Tensor& w, const Tensor& out, const optiona
               const optional<Tensor>& hn_w, const optional<Tensor>& hn_rope, at::IntArrayRef hn, double hn_eps,
               const optional<Tensor>& act_alpha, at::IntArrayRef conv) {
   gemm_launch(a, w, out, bias, epilogue, aux, gate, act, out_div, tile, hn_w, hn_rope, hn, hn_eps, act_alpha, conv);
+}
+
+// h = round(h + round(gate * (a @ w^T))), then xn = round(rmsnorm(h) * scale1 + shift): a gated residual
+// (model.py:385,388) followed by the next LowRankAdaLN's normalisation (model.py:76-81) — fused into one
+// finish kernel on under-filled launches, the two kernels otherwise (bitwise equal)
+void gemm_resid_norm_out(const Tensor& a, const Tensor& w, const Tensor& h, const optional<Tensor>& gate,
+                         const Tensor& shift, const Tensor& scale1, double eps, const Tensor& xn, int64_t tile) {
+  const ModArgs m{xn, shift, scale1, eps};
+  gemm_launch(a, w, h, c10::nullopt, ECHO_EPI_RESID, h, gate, 0, 0.0, tile, c10::nullopt, c10::nullopt, {}, 0.0,
+              c10::nullopt, {}, &m);
 }
 
 // ------------------------------------------------------------------------------------- attention
@@ -583,6 +620,8 @@ std::string version() { return std::string(echo_version()); }
 TORCH_LIBRARY(echo_hip, m) {
   m.def("gemm(Tensor a, Tensor w, " GEMM_ARGS ") -> Tensor");
   m.def("gemm_out(Tensor a, Tensor w, Tensor(a!) out, " GEMM_ARGS ") -> ()");
+  m.def("gemm_resid_norm_out(Tensor a, Tensor w, Tensor(a!) h, Tensor? gate, Tensor shift, Tensor scale1, "
+        "float eps, Tensor(b!) xn, int tile=0) -> ()");
   m.def("joint_attention(" ATTN_ARGS ", float scale=0.08838834764831845) -> Tensor");
   m.def("joint_attention_out(" ATTN_ARGS ", Tensor(a!) out, float scale=0.08838834764831845) -> ()");
   m.def("attention_variant_out(" ATTN_ARGS ", Tensor(a!) out, float scale, int variant, int ablation, "
@@ -616,6 +655,7 @@ TORCH_LIBRARY(echo_hip, m) {
 TORCH_LIBRARY_IMPL(echo_hip, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("gemm_out", &gemm_out);
+  m.impl("gemm_resid_norm_out", &gemm_resid_norm_out);
   m.impl("joint_attention", &joint_attention);
   m.impl("joint_attention_out", &joint_attention_out);
   m.impl("attention_variant_out", &attention_variant_out);
@@ -641,7 +681,7 @@ TORCH_LIBRARY_IMPL(echo_hip, CUDA, m) {
 }
 
 TORCH_LIBRARY_IMPL(echo_hip, CPU, m) {
-  for (const char* name : {"gemm", "gemm_out", "joint_attention", "joint_attention_out", "attention_variant_out",
+  for (const char* name : {"gemm", "gemm_out", "gemm_resid_norm_out", "joint_attention", "joint_attention_out", "attention_variant_out",
                            "rmsnorm", "rmsnorm_out", "norm_modulate", "norm_modulate_out", "head_norm_rope_",
                            "timestep_embedding", "silu", "silu_out", "adaln_finish", "adaln_finish_out",
                            "latent_to_input", "latent_to_input_out", "euler_cfg_step", "euler_cfg_step_", "embed",

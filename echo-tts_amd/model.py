@@ -404,16 +404,22 @@ class EchoDiTHip:
         M = R * N
         ops.gemm(ws.xin, self.w_in, out=ws.h, bias=self.b_in)
         share0 = copies > 1 and not per_row_tab and SHARE_LAYER0 and R % copies == 0
-        for i in range(len(self.layers)):
-            self.decoder_layer(ws, i, R, N, tab, segs if not callable(segs) else segs(i), start_pos, per_row_tab,
-                               share_copies=copies if (i == 0 and share0) else 1)
+        nl = len(self.layers)
+        xn_ready = False
+        for i in range(nl):
+            # layer i's closing residual also writes layer i+1's attention AdaLN (ops.gemm_resid_norm)
+            nxt = None if (per_row_tab or i + 1 == nl) else (tab[2 * i + 2, 0], tab[2 * i + 2, 1])
+            xn_ready = self.decoder_layer(ws, i, R, N, tab, segs if not callable(segs) else segs(i), start_pos,
+                                          per_row_tab, share_copies=copies if (i == 0 and share0) else 1,
+                                          xn_ready=xn_ready, next_mod=nxt)
         eps = self.cfg.norm_eps
         ops.rmsnorm(ws.h, self.out_norm, eps, out=ws.xn)
         ops.gemm(ws.xn, self.w_out, out=ws.v, bias=self.b_out, epilogue=L.EPI_F32OUT)
         return ws.v[:M]
 
     def decoder_layer(self, ws: Workspace, i: int, R: int, N: int, tab: Tensor, segs: Sequence,
-                      start_pos: int = 0, per_row_tab: bool = False, share_copies: int = 1) -> None:
+                      start_pos: int = 0, per_row_tab: bool = False, share_copies: int = 1, xn_ready: bool = False,
+                      next_mod: Optional[Tuple[Tensor, Tensor]] = None) -> bool:
         """TransformerBlock.forward (model.py:371-390) of layer i, in place on ws.h [R*N, D] (bf16
         residual stream): x += g_a * Attn(AdaLN_a(x)); x += g_m * MLP(AdaLN_m(x)).
 
@@ -424,7 +430,12 @@ class EchoDiTHip:
         group only — its q/k/v/gate are those of every group — and ONE attention launch over all R
         rows reads that group's q/gate/self K/V for every row (q row r % Rg, `EchoAttnArgs.q_batch_mod`)
         with each row's own text/speaker lengths: the same launch shape, split-KV choice and per-row
-        arithmetic as the unshared layer, so the result is bitwise equal."""
+        arithmetic as the unshared layer, so the result is bitwise equal.
+
+        The AdaLN that follows each gated residual is issued with it (ops.gemm_resid_norm: one finish kernel
+        on under-filled launches, bitwise the two-kernel result): the MLP's always, and with next_mod =
+        (shift, scale1) of layer i+1's attention AdaLN also the next layer's, which is then called with
+        xn_ready=True (ws.xn already holds it). Returns whether ws.xn holds that next-layer input."""
         cfg = self.cfg
         D, H, eps = cfg.model_size, cfg.num_heads, cfg.norm_eps
         lay = self.layers[i]
@@ -439,7 +450,8 @@ class EchoDiTHip:
                 sh, s1, g = tab[2 * i + a, 0], tab[2 * i + a, 1], tab[2 * i + a, 2]
             if a == 0:
                 Mg = Rg * N
-                ops.adaln_modulate(ws.h[:Mg], sh, s1, eps, ws.xn[:Mg])
+                if not xn_ready:
+                    ops.adaln_modulate(ws.h[:Mg], sh, s1, eps, ws.xn[:Mg])
                 # QKVG projection with q/k RMSNorm + half RoPE fused into its epilogue
                 ops.gemm(ws.xn[:Mg], lay.wqkvg, out=ws.qkvg[:Mg],
                          head_norm=ops.HeadNorm(lay.qk_norm, H, 2, eps, w_stride=H * 128, rope=self.rope,
@@ -449,14 +461,20 @@ class EchoDiTHip:
                 ops.attention(qg[:, :, 0], [self_seg] + cond_segs, out=og4, gate=qg[:, :, 3])
                 src, w = ws.og, lay.wo
             else:
-                ops.adaln_modulate(ws.h, sh, s1, eps, ws.xn)
+                if per_row_tab:
+                    ops.adaln_modulate(ws.h, sh, s1, eps, ws.xn)
                 ops.gemm(ws.xn, lay.w13, out=ws.u, epilogue=L.EPI_SWIGLU)
                 src, w = ws.u, lay.w2
             if per_row_tab:
                 h3 = ws.h.view(R, N, D)
                 ops.gemm(src.view(R, N, -1), w, out=h3, epilogue=L.EPI_RESID, aux=h3, gate=g)
-            else:
+                continue
+            nm = (tab[2 * i + 1, 0], tab[2 * i + 1, 1]) if a == 0 else next_mod
+            if nm is None:
                 ops.gemm(src, w, out=ws.h, epilogue=L.EPI_RESID, aux=ws.h, gate=g)
+            else:
+                ops.gemm_resid_norm(src, w, ws.h, g, nm[0], nm[1], eps, ws.xn)
+        return next_mod is not None and not per_row_tab
 
     # ------------------------------------------------------------------ generic forward (API)
     @torch.no_grad()

@@ -104,6 +104,17 @@ def gemm(a: Tensor, w: Tensor, out: Optional[Tensor] = None, *, bias: Optional[T
     return out
 
 
+def gemm_resid_norm(a: Tensor, w: Tensor, h: Tensor, gate: Optional[Tensor], shift: Tensor, scale1: Tensor,
+                    eps: float, xn: Tensor, tile: int = 0) -> Tensor:
+    """h = round(h + round(gate * (a @ w^T))) in place, then xn = adaln_modulate(h, shift, scale1, eps) —
+    the gated residual of a TransformerBlock (model.py:385,388) and the next LowRankAdaLN's normalisation
+    (model.py:76-81) as one call (torch.ops.echo_hip.gemm_resid_norm_out). Under-filled launches run the
+    normalisation inside the GEMM's split-K finish kernel; the result is bitwise that of
+    `gemm(..., epilogue=EPI_RESID)` + `adaln_modulate` either way."""
+    T().gemm_resid_norm_out(a, w, h, gate, shift, scale1, eps, xn, tile)
+    return xn
+
+
 @dataclass
 class Segment:
     """One KV segment: k, v views [Bk, L, H, 128] (head_dim contiguous, same strides)."""
@@ -344,7 +355,7 @@ def _register_fakes() -> None:
     def _noop(*args, **kwargs):
         return None
 
-    for name in ("gemm_out", "joint_attention_out", "attention_variant_out", "rmsnorm_out", "norm_modulate_out",
+    for name in ("gemm_out", "gemm_resid_norm_out", "joint_attention_out", "attention_variant_out", "rmsnorm_out", "norm_modulate_out",
                  "head_norm_rope_", "silu_out", "adaln_finish_out", "latent_to_input_out", "euler_cfg_step_",
                  "embed_out", "scale_rows_", "cast_from_f32_out"):
         reg(f"echo_hip::{name}", _noop)

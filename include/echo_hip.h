@@ -76,6 +76,14 @@ typedef struct {
    * Rows before t = 0 are read from memory: the caller keeps >= (conv_taps-1)*conv_dil zero rows
    * ahead of A. conv_c % 64 == 0 (bf16) / % 16 == 0 (fp32). */
   int32_t conv_c, conv_taps, conv_dil;
+  /* ECHO_EPI_RESID only, mod_out != NULL: also the NEXT LowRankAdaLN normalisation of the updated rows,
+   *   mod_out[m][n] = round(((out[m][n] * rsqrt(mean_n(out[m][:]^2) + mod_eps)) * mod_scale1[n]) + mod_shift[n])
+   * (echo_adaln_modulate's arithmetic on the residual stream this GEMM just wrote; model.py:76-81 of the next
+   * AdaLN). Fused into the split-K finish kernel of under-filled launches (N == 2048: one workgroup per row),
+   * a separate echo_adaln_modulate pass after the GEMM otherwise; bitwise the same either way. */
+  void* mod_out; int64_t ld_mod;
+  const void* mod_shift; const void* mod_scale1;
+  float mod_eps;
 } EchoGemmArgs;
 
 /* Replaces every nn.Linear of the DiT and its encoders (F.linear, model.py:56-62,
@@ -311,9 +319,10 @@ int echo_rvq_encode(int32_t dtype, const void* z, int64_t ldz, int32_t rows, int
 const char* echo_version(void);
 
 /* ABI revision of the argument structs in this header. Bumped whenever a struct's layout changes
- * (4: EchoAttnArgs gained the trailing q_batch_mod). A binding built against an older header must
+ * (4: EchoAttnArgs gained the trailing q_batch_mod; 5: EchoGemmArgs gained the mod_* fields of the fused
+ * residual + AdaLN). A binding built against an older header must
  * refuse to run: check echo_abi_version() == ECHO_ABI_VERSION and the struct sizes below at load. */
-#define ECHO_ABI_VERSION 4
+#define ECHO_ABI_VERSION 5
 int32_t echo_abi_version(void);
 /* sizeof() of an argument struct as this library was compiled: 0 EchoGemmArgs, 1 EchoAttnArgs,
  * 2 EchoKVSegment, 3 EchoStepArgs, 4 EchoRvqWeights; -1 for an unknown id. */

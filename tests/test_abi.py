@@ -122,7 +122,7 @@ def test_gemm_tile_pick_host_policy(lib):
     assert pick(1920, 2048, 5888, 1) == 4    # C2 CFG residual, 64 tiles -> 128x64
 
 
-TORCH_OPS = ("gemm", "gemm_out", "joint_attention", "joint_attention_out", "attention_variant_out", "rmsnorm",
+TORCH_OPS = ("gemm", "gemm_out", "gemm_resid_norm_out", "joint_attention", "joint_attention_out", "attention_variant_out", "rmsnorm",
              "rmsnorm_out", "norm_modulate", "norm_modulate_out", "head_norm_rope_", "timestep_embedding", "silu",
              "silu_out", "adaln_finish", "adaln_finish_out", "latent_to_input", "latent_to_input_out",
              "euler_cfg_step", "euler_cfg_step_", "embed", "embed_out", "scale_rows_", "cast_from_f32",

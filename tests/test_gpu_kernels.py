@@ -916,6 +916,50 @@ def test_gemm_small_m_policy_rows():
     assert lib.echo_set_policy_rows(1, 2) != 0 and lib.echo_set_policy_rows(0, 1) != 0
 
 
+@pytest.mark.parametrize("M,K", [(160, 2048), (160, 5888), (480, 5888), (640, 2048), (640, 5888), (1920, 2048),
+                                 (333, 5888)])
+def test_gemm_resid_norm_bitwise(M, K):
+    """ops.gemm_resid_norm (gated residual + the next AdaLN; the finish kernel's fused normalisation where
+    the small-M plan has a finish kernel, GEMM + adaln_modulate otherwise) is bitwise the two-call
+    sequence gemm(EPI_RESID) + adaln_modulate — h and xn — for the auto plan (split and unsplit shapes, a
+    ragged M, a large-M fallback), forced split configs, a direct-epilogue config and N = 1024."""
+    N, eps = 2048, 1e-5
+    torch.manual_seed(M + K)
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.03).to(BF)
+    h0 = torch.randn(M, N, device=DEV).to(BF)
+    g = (torch.rand(N, device=DEV) + 0.5).to(BF)
+    sh = (torch.randn(N, device=DEV) * 0.1).to(BF)
+    s1 = (torch.rand(N, device=DEV) + 0.5).to(BF)
+
+    def two(tile):
+        h = h0.clone()
+        ops.gemm(a, w, out=h, epilogue=L.EPI_RESID, aux=h, gate=g, tile=tile)
+        return h, ops.adaln_modulate(h, sh, s1, eps)
+
+    def one(tile, wv=w, gv=g, shv=sh, s1v=s1, hv=h0):
+        h = hv.clone()
+        xn = torch.empty_like(h)
+        ops.gemm_resid_norm(a, wv, h, gv, shv, s1v, eps, xn, tile=tile)
+        return h, xn
+
+    for tile in (0, 132, 164, 131, 183):  # auto; cfg 3 S2; cfg 6 S4; cfg 3 unsplit (direct); cfg 8 S3
+        rh, rx = two(tile)
+        fh, fx = one(tile)
+        assert torch.equal(fh, rh), tile
+        assert torch.equal(fx, rx), tile
+    # N = 1024 (the finish workgroup is not a row): GEMM + adaln_modulate
+    h1 = h0[:, :1024].contiguous()
+    hr = h1.clone()
+    ops.gemm(a, w[:1024], out=hr, epilogue=L.EPI_RESID, aux=hr, gate=g[:1024], tile=132)
+    fh, fx = one(132, w[:1024].contiguous(), g[:1024].contiguous(), sh[:1024].contiguous(), s1[:1024].contiguous(),
+                 h1)
+    assert torch.equal(fh, hr)
+    assert torch.equal(fx, ops.adaln_modulate(hr, sh[:1024].contiguous(), s1[:1024].contiguous(), eps))
+    with pytest.raises(RuntimeError):  # shift must be [N]
+        ops.gemm_resid_norm(a, w, h0.clone(), g, sh[:1024], s1, eps, torch.empty_like(h0))
+
+
 def test_gemm_headnorm_rejects_bad_args():
     a = torch.randn(64, 64, device=DEV).to(BF)
     w = torch.randn(512, 64, device=DEV).to(BF)
