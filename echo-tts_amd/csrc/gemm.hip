@@ -92,6 +92,12 @@ __device__ __forceinline__ float xor_lane16(float x) {
   else return __int_as_float(__builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));
 }
 
+constexpr int largest_divisor_le(int n, int cap) {
+  int d = cap < n ? cap : n;
+  while (n % d) --d;
+  return d;
+}
+
 // Epilogue shared by the bf16 kernels (must follow a barrier after the last LDS read):
 // stage 1 registers -> per-wave swizzled LDS tile (bf16-rounded, bias/act/div or SwiGLU);
 // stage 2 16-B row chunks -> residual/gate tail -> coalesced stores.
@@ -237,7 +243,8 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
     // the long-latency loads overlap; in-place residual (aux == C) is safe because every
     // element is read and written by the same lane.
     constexpr int CHc = (EK == EK_SWIGLU ? TN / 2 : TN) / 8, RPIc = 64 / CHc, NIT = TM / RPIc;
-    constexpr int NB = (EK == EK_RESID || NIT > 16) ? (NIT < 8 ? NIT : 8) : NIT;  // row chunks per batch (registers)
+    // row chunks per batch (registers): all of them, or at most 8 (residual / long tiles) — a divisor of NIT
+    constexpr int NB = (EK == EK_RESID || NIT > 16) ? largest_divisor_le(NIT, 8) : NIT;
     const int c = lane % CHc;
     const int n = nbase + c * 8;
     if (n >= Nout) return;
@@ -2438,8 +2445,13 @@ constexpr SkCfg kSk[] = {
     {128, 64, 2, 4, 4},   //      under the other's MFMAs)
     {64, 64, 2, 4, 4},
     {64, 128, 2, 4, 4},
+    {160, 128, 2, 2, 4},  // 10: 144 KB; 11: 156 KB; 12: 144 KB — whole 160-row blocks / wide tiles for the
+    {160, 256, 2, 2, 3},  //     weight-streaming launches (QKVG / W13 at 160-640 rows: few, big, K-split
+    {128, 256, 2, 2, 3},  //     tiles cut the per-CU re-read of A)
 };
-constexpr int kNumSk = 9;
+constexpr int kNumSk = 12;
+// `tile` 100 + 10 c + S (c = 1 .. kNumSk, S = 1 .. 9): small-M config c with K split S
+constexpr bool sk_tile(int t) { return t >= 110 && t < 100 + 10 * (kNumSk + 1) && t % 10 != 0; }
 int sk_occ(int c) { return (160 * 1024) / ((kSk[c].bm + kSk[c].bn) * BK * 2 * kSk[c].ns); }
 
 // the fused epilogue straight from the unit's registers is expressible for this wave tile (gemm_epilogue's
@@ -2561,6 +2573,9 @@ int launch_sk_cfg(const EchoGemmArgs* a, const Epi& ep, int c, int S, void* ws, 
     case 7: return launch_sk<128, 64, 2, 4, 4>(a, ep, S, ws, s);
     case 8: return launch_sk<64, 64, 2, 4, 4>(a, ep, S, ws, s);
     case 9: return launch_sk<64, 128, 2, 4, 4>(a, ep, S, ws, s);
+    case 10: return launch_sk<160, 128, 2, 2, 4>(a, ep, S, ws, s);
+    case 11: return launch_sk<160, 256, 2, 2, 3>(a, ep, S, ws, s);
+    case 12: return launch_sk<128, 256, 2, 2, 3>(a, ep, S, ws, s);
     default: return ECHO_EINVAL;
   }
 }
@@ -2599,8 +2614,8 @@ extern "C" int echo_set_policy_rows(int32_t num, int32_t den) {
 
 extern "C" int64_t echo_gemm_ws_bytes(const EchoGemmArgs* a) {
   if (!a || a->M <= 0 || a->N <= 0 || a->K <= 0 || a->K % BK) return 0;
-  if (a->tile >= 110 && a->tile <= 199) {
-    const int c = (a->tile / 10) % 10, S = a->tile % 10;
+  if (sk_tile(a->tile)) {
+    const int c = (a->tile - 100) / 10, S = a->tile % 10;
     if (c < 1 || c > kNumSk || S < 1 || !sk_ok(a)) return 0;
     return sk_ws_bytes(a, c, S);
   }
@@ -2644,19 +2659,20 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
     // residual + the next AdaLN: fused into the finish kernel when the small-M plan has one (K split or
     // no direct epilogue) and a row is one finish workgroup (N == 2048); else the GEMM, then
     // echo_adaln_modulate on the rows it wrote (the same kernel arithmetic: bitwise equal)
-    if (a->epilogue != ECHO_EPI_RESID || a->dtype != ECHO_BF16 || a->batch != 1 || !a->mod_shift ||
-        !a->mod_scale1 || a->ldc != a->N || a->ld_mod != a->N || (a->N != 1024 && a->N != 2048 && a->N != 4096) ||
-        ((uintptr_t)a->mod_out | (uintptr_t)a->mod_shift | (uintptr_t)a->mod_scale1) & 15)
+    if (a->epilogue != ECHO_EPI_RESID || a->batch != 1 || !a->mod_shift || !a->mod_scale1 || a->ldc != a->N ||
+        a->ld_mod != a->N)
       return ECHO_EINVAL;
+    const bool aligned = (((uintptr_t)a->mod_out | (uintptr_t)a->mod_shift | (uintptr_t)a->mod_scale1) & 15) == 0;
     int c = 0, S = 1;
-    if (a->tile >= 110 && a->tile <= 199) {
-      c = (a->tile / 10) % 10;
+    if (sk_tile(a->tile)) {
+      c = (a->tile - 100) / 10;
       S = a->tile % 10;
     } else if (a->tile != 0 || !sk_plan(a, ws != nullptr, &c, &S)) {
       c = 0;
     }
     const int64_t need = c >= 1 && c <= kNumSk && sk_ok(a) ? sk_ws_bytes(a, c, S) : 0;
-    if (a->N == 2048 && need > 0 && a->K / BK >= S && ws && (uintptr_t)ws % 16 == 0 && ws_bytes >= need) {
+    if (a->dtype == ECHO_BF16 && a->N == 2048 && aligned && need > 0 && a->K / BK >= S && ws &&
+        (uintptr_t)ws % 16 == 0 && ws_bytes >= need) {
       Epi em = ep;
       em.mod_out = a->mod_out;
       em.ld_mod = a->ld_mod;
@@ -2669,12 +2685,12 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
     b.mod_out = nullptr;
     const int rc = echo_gemm_ws(&b, ws, ws_bytes, stream);
     if (rc) return rc;
-    return echo_adaln_modulate(ECHO_BF16, a->C, a->mod_out, a->M, a->N, a->mod_shift, a->mod_scale1, 0, 0,
+    return echo_adaln_modulate(a->dtype, a->C, a->mod_out, a->M, a->N, a->mod_shift, a->mod_scale1, 0, 0,
                                a->mod_eps, stream);
   }
   // small-M family (gemm_bf16_sk_kernel): forced (`tile` 1CS) or the auto pick of under-filled launches
-  if (a->tile >= 110 && a->tile <= 199) {
-    const int c = (a->tile / 10) % 10, S = a->tile % 10;
+  if (sk_tile(a->tile)) {
+    const int c = (a->tile - 100) / 10, S = a->tile % 10;
     if (c < 1 || c > kNumSk || S < 1 || !sk_ok(a) || a->K / BK < S) return ECHO_EINVAL;
     const int64_t need = sk_ws_bytes(a, c, S);
     if (need > 0 && (!ws || (uintptr_t)ws % 16 || ws_bytes < need)) return ECHO_EINVAL;

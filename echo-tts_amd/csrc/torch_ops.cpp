@@ -223,9 +223,8 @@ void gemm_launch(const Tensor& a, const Tensor& w, const Tensor& out, const opti
     need_dev(a, mod->shift, "shift");
     need_dev(a, mod->scale1, "scale1");
     TORCH_CHECK(epilogue == ECHO_EPI_RESID && s.batch == 1 && out.is_contiguous() && mod->xn.is_contiguous() &&
-                    mod->xn.sizes() == out.sizes() && mod->xn.scalar_type() == a.scalar_type() &&
-                    a.scalar_type() == at::kBFloat16,
-                "echo_hip.gemm_resid_norm: bf16, one batch, contiguous h / xn of equal shape");
+                    mod->xn.sizes() == out.sizes() && mod->xn.scalar_type() == a.scalar_type(),
+                "echo_hip.gemm_resid_norm: one batch, contiguous h / xn of equal shape and the model dtype");
     for (const Tensor* v : {&mod->shift, &mod->scale1})
       TORCH_CHECK(v->dim() == 1 && v->numel() == s.N && v->is_contiguous() && v->scalar_type() == a.scalar_type(),
                   "echo_hip.gemm_resid_norm: shift / scale1 must be contiguous [N] of the model dtype");

@@ -79,8 +79,9 @@ typedef struct {
   /* ECHO_EPI_RESID only, mod_out != NULL: also the NEXT LowRankAdaLN normalisation of the updated rows,
    *   mod_out[m][n] = round(((out[m][n] * rsqrt(mean_n(out[m][:]^2) + mod_eps)) * mod_scale1[n]) + mod_shift[n])
    * (echo_adaln_modulate's arithmetic on the residual stream this GEMM just wrote; model.py:76-81 of the next
-   * AdaLN). Fused into the split-K finish kernel of under-filled launches (N == 2048: one workgroup per row),
-   * a separate echo_adaln_modulate pass after the GEMM otherwise; bitwise the same either way. */
+   * AdaLN). Needs batch == 1 and contiguous rows (ldc == ld_mod == N). Fused into the split-K finish kernel
+   * of under-filled bf16 launches (N == 2048: one workgroup per row), a separate echo_adaln_modulate pass
+   * after the GEMM otherwise; bitwise the same either way. */
   void* mod_out; int64_t ld_mod;
   const void* mod_shift; const void* mod_scale1;
   float mod_eps;
@@ -126,7 +127,7 @@ int echo_set_policy_rows(int32_t num, int32_t den);
  * force either form for any epilogue) (A/B timing, tools/bench_streams.py --diag; all bitwise-equal).
  * key 11: 1 = never split K in echo_gemm_ws (the B = 1 runs that tests compare bitwise with B = 16 rows);
  * key 12: 1 = no small-M kernel in the auto pick (the round-3 small tiles; A/B).
- * `tile` 1CS (C = small-M config 1..6, S = split 1..9) forces a small-M launch (tools/bench_gemm.py). */
+ * `tile` 100 + 10*C + S (C = small-M config 1..12, S = split 1..9) forces a small-M launch (tools/bench_gemm.py). */
 int echo_gemm_set_diag(int32_t key, int32_t value);
 
 /* One key/value segment of the joint attention (model.py:246-253): rows of

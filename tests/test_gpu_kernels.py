@@ -825,7 +825,7 @@ def test_gemm_headnorm_t320(M, H, pos0, rh, K):
         assert torch.equal(got, ref), tile
 
 
-SK_CFGS = (1, 2, 3, 4, 5, 6, 7, 8, 9)
+SK_CFGS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12)
 
 
 def _sk_case(M, N, K, epi, seed=0):
@@ -937,10 +937,10 @@ def test_gemm_resid_norm_bitwise(M, K):
         ops.gemm(a, w, out=h, epilogue=L.EPI_RESID, aux=h, gate=g, tile=tile)
         return h, ops.adaln_modulate(h, sh, s1, eps)
 
-    def one(tile, wv=w, gv=g, shv=sh, s1v=s1, hv=h0):
+    def one(tile, wv=w, gv=g, shv=sh, s1v=s1, hv=h0, av=a):
         h = hv.clone()
         xn = torch.empty_like(h)
-        ops.gemm_resid_norm(a, wv, h, gv, shv, s1v, eps, xn, tile=tile)
+        ops.gemm_resid_norm(av, wv, h, gv, shv, s1v, eps, xn, tile=tile)
         return h, xn
 
     for tile in (0, 132, 164, 131, 183):  # auto; cfg 3 S2; cfg 6 S4; cfg 3 unsplit (direct); cfg 8 S3
@@ -958,6 +958,13 @@ def test_gemm_resid_norm_bitwise(M, K):
     assert torch.equal(fx, ops.adaln_modulate(hr, sh[:1024].contiguous(), s1[:1024].contiguous(), eps))
     with pytest.raises(RuntimeError):  # shift must be [N]
         ops.gemm_resid_norm(a, w, h0.clone(), g, sh[:1024], s1, eps, torch.empty_like(h0))
+    # fp32 (parity mode): GEMM + the generic modulate kernel
+    af, wf, hf, gf, shf, s1f = (t.float() for t in (a, w[:512], h0[:, :512], g[:512], sh[:512], s1[:512]))
+    hr = hf.clone()
+    ops.gemm(af, wf, out=hr, epilogue=L.EPI_RESID, aux=hr, gate=gf)
+    fh, fx = one(0, wf.contiguous(), gf.contiguous(), shf.contiguous(), s1f.contiguous(), hf.contiguous(), af)
+    assert torch.equal(fh, hr)
+    assert torch.equal(fx, ops.adaln_modulate(hr, shf.contiguous(), s1f.contiguous(), eps))
 
 
 def test_gemm_headnorm_rejects_bad_args():
