@@ -5,8 +5,11 @@ rule 24), random operands, HIP events on the launch stream. Also checks that eac
 config's output is bitwise equal to config 1 (same K accumulation order).
     python tools/bench_gemm.py [--tiles 1,6] [--rounds 5]
 Tile -8: the auto pick with the column split of 320-row launches off (echo_gemm_set_diag key 8).
-Tile 1CS: the small-M kernel, config C (1..6), K split S (1..9); split outputs differ from the unsplit
-order by fp32 rounding (printed as rel-L2 against the first tile).
+Tile 100 + 10 C + S: the small-M kernel, config C (1..12), K split S (1..9); split outputs differ from the
+unsplit order by fp32 rounding (printed as rel-L2 against the first tile).
+--wcopies C: the timed launches rotate over C copies of the weight matrix, so that (C x its bytes > the
+256 MB Infinity Cache) every launch streams its weights from HBM as the decoder's 24 layers do in the
+sampler; without it the weights stay cache-resident and weight-streaming shapes look faster than in-model.
 """
 import argparse
 import os
@@ -69,6 +72,7 @@ def main():
     ap.add_argument("--no-ns3", action="store_true", help="2-stage pipeline for the small tiles (A/B)")
     ap.add_argument("--bias", action="store_true", help="add a bias vector (generic epilogue kind)")
     ap.add_argument("--stagger", type=int, default=0, help="tile 14: first-round group delay (10 ns ticks)")
+    ap.add_argument("--wcopies", type=int, default=1, help="rotate over this many weight copies (HBM streaming)")
     args = ap.parse_args()
     if args.stagger:
         assert L.load().echo_gemm_set_diag(1, args.stagger) == 0
@@ -90,6 +94,7 @@ def main():
     for name, M, N, K, epi in shapes:
         a = torch.randn(M, K + args.pad_a, device=dev).to(torch.bfloat16)[:, :K]
         w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+        ws = [w] + [w.clone() for _ in range(args.wcopies - 1)]
         nout = N // 2 if epi == L.EPI_SWIGLU else N
         aux = torch.randn(M, nout, device=dev).to(torch.bfloat16)
         gate = torch.randn(nout, device=dev).to(torch.bfloat16) if epi == L.EPI_RESID else None
@@ -111,9 +116,9 @@ def main():
             for t in tiles:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                for _ in range(args.iters):
-                    gemm_t(a, w, t, out=out, epilogue=epi, aux=aux if epi == L.EPI_RESID else None, gate=gate,
-                           bias=bias)
+                for i in range(args.iters):
+                    gemm_t(a, ws[i % len(ws)], t, out=out, epilogue=epi, aux=aux if epi == L.EPI_RESID else None,
+                           gate=gate, bias=bias)
                 e1.record()
                 torch.cuda.synchronize()
                 times[t].append(e0.elapsed_time(e1) / args.iters)
@@ -124,8 +129,8 @@ def main():
             for _ in range(args.rounds):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                for _ in range(args.iters):
-                    torch.nn.functional.linear(a, w)
+                for i in range(args.iters):
+                    torch.nn.functional.linear(a, ws[i % len(ws)])
                 e1.record()
                 torch.cuda.synchronize()
                 ts.append(e0.elapsed_time(e1) / args.iters)
