@@ -159,8 +159,9 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
     // (wm, 2p+1) (TN == 64; each wave of the pair then takes half of the pair's rows). 16 lanes
     // per row, 8 consecutive columns per lane and the same xor-butterfly sum as
     // head_norm_rope_kernel, so results are bitwise equal.
-    static_assert((TN == 64 || TN == 128) && TM == 128, "HEADNORM epilogue is for the 256x256 kernels");
+    static_assert((TN == 64 || TN == 128) && TM % 8 == 0, "HEADNORM epilogue: 64- or 128-column wave tiles");
     constexpr bool PAIR = TN == 64;
+    constexpr int PR = PAIR ? TM / 2 : 0;  // rows of the pair's tile taken by the second wave
     constexpr int CHS = TN / 8;  // 16-B chunks per staged row
     if (PAIR) __syncthreads();   // the partner wave's staged tile is complete
     const int hcol = n0 + (PAIR ? (wn & ~1) : wn) * TN;  // first column of this wave's head
@@ -175,16 +176,16 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
     if (norm) load8((const bf16_t*)ep.hn_w + blk * ep.hn_w_stride + h * 128 + ch * 8, wv);
     bf16_t* Cp = (bf16_t*)Cv + z * sC + hcol + ch * 8;
     if (hcol >= N) return;
-    constexpr int NR = PAIR ? 16 : 32;  // 4-row iterations per wave
+    constexpr int NR = (PAIR ? TM / 2 : TM) / 4;  // 4-row iterations per wave
     // Batched: the LDS reads, RoPE table loads, sums, butterflies and reciprocal square roots of
     // HB row iterations are issued together (independent chains interleave) instead of one
     // row iteration's serial chain at a time; per element the same operations in the same order.
-    constexpr int HB = 4;
+    constexpr int HB = largest_divisor_le(NR, 4);
     for (int it0 = 0; it0 < NR; it0 += HB) {
       float v[HB][8];
 #pragma unroll
       for (int b = 0; b < HB; ++b) {
-        const int row = (PAIR ? (wn & 1) * 64 : 0) + (it0 + b) * 4 + rq;
+        const int row = (wn & 1) * PR + (it0 + b) * 4 + rq;
         load8(src + row * TN + ((c ^ (row & (CHS - 1))) * 8), v[b]);
       }
       if (norm) {
@@ -192,7 +193,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
         if (rope) {
 #pragma unroll
           for (int b = 0; b < HB; ++b) {
-            const int m = m0 + wm * TM + (PAIR ? (wn & 1) * 64 : 0) + (it0 + b) * 4 + rq;
+            const int m = m0 + wm * TM + (wn & 1) * PR + (it0 + b) * 4 + rq;
             const int pos = ep.hn_pos0 + ep.hn_pos_mult * (min(m, M - 1) % ep.hn_seq_len);
             const float4* cp = (const float4*)(ep.hn_rope + ((int64_t)pos * 64 + ch * 4) * 2);
             cs[b][0] = cp[0];
@@ -233,7 +234,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
       }
 #pragma unroll
       for (int b = 0; b < HB; ++b) {
-        const int m = m0 + wm * TM + (PAIR ? (wn & 1) * 64 : 0) + (it0 + b) * 4 + rq;
+        const int m = m0 + wm * TM + (wn & 1) * PR + (it0 + b) * 4 + rq;
         if (m < M) store8(Cp + (int64_t)m * ldc, v[b]);
       }
     }
@@ -2457,9 +2458,11 @@ int sk_occ(int c) { return (160 * 1024) / ((kSk[c].bm + kSk[c].bn) * BK * 2 * kS
 // the fused epilogue straight from the unit's registers is expressible for this wave tile (gemm_epilogue's
 // row-chunk loop must divide the wave's rows); otherwise the launch goes through the finish kernel
 constexpr bool sk_direct(int tm, int tn, int ek) {
-  // SwiGLU pairs the w1 / w3 16-column blocks inside a wave: its tile needs whole pairs (tn % 32 == 0)
-  return ek == EK_SWIGLU ? (tn % 32 == 0 && tm % (64 / (tn / 16)) == 0)
-                         : (ek == EK_STORE || ek == EK_RESID) && tm % (64 / (tn / 8)) == 0;
+  // SwiGLU pairs the w1 / w3 16-column blocks inside a wave: its tile needs whole pairs (tn % 32 == 0);
+  // head norm: a 128-column head in one wave's tile or in a pair of waves' 64-column tiles
+  return ek == EK_SWIGLU     ? (tn % 32 == 0 && tm % (64 / (tn / 16)) == 0)
+         : ek == EK_HEADNORM ? ((tn == 64 || tn == 128) && tm % 8 == 0)
+                             : (ek == EK_STORE || ek == EK_RESID) && tm % (64 / (tn / 8)) == 0;
 }
 
 // small-M path applies: bf16, one batch, no conv, a fused kind the finish kernel has, 32-bit DMA offsets
@@ -2477,7 +2480,7 @@ bool sk_ok(const EchoGemmArgs* a) {
 
 bool sk_partial(int c, int S, int ek) {
   const int tm = kSk[c].bm / kSk[c].wm, tn = kSk[c].bn / kSk[c].wn;
-  return S > 1 || ek == EK_HEADNORM || !sk_direct(tm, tn, ek);
+  return S > 1 || !sk_direct(tm, tn, ek);
 }
 
 int64_t sk_ws_bytes(const EchoGemmArgs* a, int c, int S) {
@@ -2532,11 +2535,12 @@ int launch_sk(const EchoGemmArgs* a, const Epi& ep, int S, void* ws, hipStream_t
   const int ek = ek_of(a);
   const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;
   const bool mod = ep.mod_out != nullptr;  // caller checked: RESID, N == 2048, partial plan
-  if (!mod && !(S > 1 || ek == EK_HEADNORM || !sk_direct(BM / WM, BN / WN, ek))) {
+  if (!mod && !(S > 1 || !sk_direct(BM / WM, BN / WN, ek))) {
     switch (ek) {
       case EK_STORE: return launch_sk_direct<BM, BN, WM, WN, NS, EK_STORE>(a, ep, s);
       case EK_SWIGLU: return launch_sk_direct<BM, BN, WM, WN, NS, EK_SWIGLU>(a, ep, s);
       case EK_RESID: return launch_sk_direct<BM, BN, WM, WN, NS, EK_RESID>(a, ep, s);
+      case EK_HEADNORM: return launch_sk_direct<BM, BN, WM, WN, NS, EK_HEADNORM>(a, ep, s);
       default: return ECHO_EINVAL;
     }
   }

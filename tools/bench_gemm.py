@@ -99,11 +99,20 @@ def main():
         aux = torch.randn(M, nout, device=dev).to(torch.bfloat16)
         gate = torch.randn(nout, device=dev).to(torch.bfloat16) if epi == L.EPI_RESID else None
         bias = torch.randn(nout, device=dev).to(torch.bfloat16) if args.bias else None
+        hn = None
+        if epi == L.EPI_HEADNORM:  # QKVG: q/k RMSNorm + half RoPE over the first 2 of 4 head blocks
+            from echo_tts_amd.model import rope_table_cpu
+            H = N // 512
+            nw = (1 + 0.1 * torch.randn(2, H, 128, device=dev)).to(torch.bfloat16)
+            hn = ops.HeadNorm(nw, H, 2, 1e-5, w_stride=H * 128, rope=rope_table_cpu(128, 4096).to(dev),
+                              rope_heads=H // 2, seq_len=min(M, 640))
+            epi = L.EPI_STORE
         outs = {}
         for t in tiles:
             odt = torch.float32 if epi == L.EPI_F32OUT else torch.bfloat16
             o = aux.clone() if epi == L.EPI_RESID else torch.empty(M, nout, device=dev, dtype=odt)
-            gemm_t(a, w, t, out=o, epilogue=epi, aux=o if epi == L.EPI_RESID else None, gate=gate, bias=bias)
+            gemm_t(a, w, t, out=o, epilogue=epi, aux=o if epi == L.EPI_RESID else None, gate=gate, bias=bias,
+                   head_norm=hn)
             outs[t] = o
         base = outs[tiles[0]]
         same = {t: bool(torch.equal(outs[t], base)) for t in tiles}
@@ -118,7 +127,7 @@ def main():
                 e0.record()
                 for i in range(args.iters):
                     gemm_t(a, ws[i % len(ws)], t, out=out, epilogue=epi, aux=aux if epi == L.EPI_RESID else None,
-                           gate=gate, bias=bias)
+                           gate=gate, bias=bias, head_norm=hn)
                 e1.record()
                 torch.cuda.synchronize()
                 times[t].append(e0.elapsed_time(e1) / args.iters)
