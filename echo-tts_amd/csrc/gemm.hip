@@ -2495,17 +2495,34 @@ int64_t policy_rows(int64_t rows) { return rows * g_policy_num / g_policy_den; }
 bool sk_plan(const EchoGemmArgs* a, bool allow_split, int* cfg, int* split) {
   if (g_gemm_no_sk || !sk_ok(a)) return false;
   const int64_t Mp = policy_rows(a->M);
-  // Measured (profiles/r4_sk_sweep.txt: every config x split against the round-3 pick and hipBLASLt, MI355X,
-  // interleaved): the small-M family wins only on the gated-residual shapes of the B = 1 / blockwise decoder
-  // (N = 2048) at up to 768 rows, where the round-3 tiles leave most CUs idle on a long K (K = 5888:
-  // M = 160 33.6 -> 16.4 us, M = 480 33.5 -> 25.7, M = 640 38.0 -> 29.5; K = 2048: 15.1 -> 11.8, 14.0 ->
-  // 12.8, 16.9 -> 15.6). Elsewhere (QKVG / W13, M = 1920) the round-3 picks are as fast or faster.
-  if (ek_of(a) != EK_RESID || a->N > 2048 || a->N < 1024 || Mp > 768) return false;
+  // Measured with the weights streamed from HBM as in the sampler (profiles/r4_sk_hbm_sweep.txt: every
+  // config x split against the round-3 pick and hipBLASLt, 16 rotating weight copies; cache-resident
+  // weights, profiles/r4_sk_sweep.txt, hide the difference): the 4-deep LDS-DMA ring keeps enough weight
+  // bytes in flight per CU where the round-3 tiles (2-stage, one K-tile ahead) wait on HBM latency.
+  //   gated residual, N = 2048 (Wo K = 2048, W2 K = 5888), us:    M = 160      480      640     1920
+  //     round-3 pick                                       K 2048  12.0     12.9     15.9     24.6
+  //                                                        K 5888  20.4     31.3     31.1     69.7
+  //     here                                               K 2048  11.8 8/2 12.5 8/1 15.8 3/1  (r3)
+  //                                                        K 5888  17.8 5/4 25.4 6/4 30.2 6/3  58.5 6/1
+  //   QKVG + q/k norm + RoPE (N = 8192; round 3: store + head_norm_rope) 22.6 -> 18.9 (5/1),
+  //     37.1 -> 27.0 (1/1), 39.5 -> 33.5 (10/1); W13 SwiGLU at 160 rows 24.4 -> 22.8 (6/1); the other W13 /
+  //     QKVG shapes keep the round-3 pick (as fast or faster there).
+  const int ek = ek_of(a);
   const bool longk = a->K >= 4096;
-  int c, S;
-  if (Mp <= 256) { c = 3; S = longk ? 4 : 2; }
-  else if (Mp <= 512) { c = longk ? 3 : 8; S = longk ? 2 : 1; }
-  else { c = longk ? 6 : 3; S = longk ? 3 : 1; }
+  int c, S = 1;
+  if (ek == EK_RESID && a->N >= 1024 && a->N <= 2048) {
+    if (Mp <= 256) { c = longk ? 5 : 8; S = longk ? 4 : 2; }
+    else if (Mp <= 512) { c = longk ? 6 : 8; S = longk ? 4 : 1; }
+    else if (Mp <= 768) { c = longk ? 6 : 3; S = longk ? 3 : 1; }
+    else if (Mp <= 2048 && longk) c = 6;
+    else return false;
+  } else if (ek == EK_HEADNORM && a->N >= 4096 && Mp <= 768) {
+    c = Mp <= 256 ? 5 : Mp <= 512 ? 1 : 10;
+  } else if (ek == EK_SWIGLU && a->N >= 8192 && Mp <= 256) {
+    c = 6;
+  } else {
+    return false;
+  }
   if (!allow_split || g_gemm_no_splitk) S = 1;
   S = std::max(1, std::min(S, a->K / BK / 2));
   *cfg = c;
