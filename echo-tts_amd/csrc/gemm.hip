@@ -1794,9 +1794,11 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
 #pragma unroll
           for (int j = 0; j < FN; ++j) asm volatile("" : "+v"(hpa[ii][j].x), "+v"(hpa[ii][j].y));
       }
+      // norm weights: PER re-reads them per row fragment (L1 hits) instead of holding 16 registers across the
+      // row loop (the persistent form's live range is what spilled)
+      const bf16_t* wp = (const bf16_t*)ep.hn_w + hblk * ep.hn_w_stride + hhd * 128 + 4 * g4;
       uint2 hw[FN];
-      if (hnorm) {
-        const bf16_t* wp = (const bf16_t*)ep.hn_w + hblk * ep.hn_w_stride + hhd * 128 + 4 * g4;
+      if (!PER && hnorm) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) hw[j] = *(const uint2*)(wp + j * 16);
       }
@@ -1804,15 +1806,21 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
       for (int ii = 0; ii < FM; ++ii) {
         const int m = mb + ii * 16;
         float4 rc[FN];
-        if (hrope) {  // (cos, sin) of the lane's 2 column pairs per fragment, in flight during the sums
-          const int pos = ep.hn_pos0 + ep.hn_pos_mult * (min(m, M - 1) % ep.hn_seq_len);
-          const float* rp = ep.hn_rope + ((int64_t)pos * 64 + 2 * g4) * 2;
+        const int pos = ep.hn_pos0 + ep.hn_pos_mult * (min(m, M - 1) % ep.hn_seq_len);
+        const float* rp = ep.hn_rope + ((int64_t)pos * 64 + 2 * g4) * 2;
+        if (!PER && hrope) {  // (cos, sin) of the lane's 2 column pairs per fragment, in flight during the sums
 #pragma unroll
           for (int j = 0; j < FN; ++j) rc[j] = *(const float4*)(rp + j * 16);
         }
         uint2 hp[FN];
 #pragma unroll
         for (int j = 0; j < FN; ++j) hp[j] = hpa[ii][j];
+        if constexpr (PER) {
+          if (hnorm) {
+#pragma unroll
+            for (int j = 0; j < FN; ++j) hw[j] = *(const uint2*)(wp + j * 16);
+          }
+        }
         if (hnorm) {
           float c8[FN];
 #pragma unroll
@@ -1848,7 +1856,7 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
             for (int j = 0; j < FN; ++j) {
               float v[4];
               unpack(hp[j], v);
-              const float4 cs = rc[j];
+              const float4 cs = PER ? *(const float4*)(rp + j * 16) : rc[j];  // PER: loaded at the use
               const float y0 = (v[0] * cs.x) - (v[1] * cs.y), y1 = (v[0] * cs.y) + (v[1] * cs.x);
               const float y2 = (v[2] * cs.z) - (v[3] * cs.w), y3 = (v[2] * cs.w) + (v[3] * cs.z);
               hp[j] = make_uint2(pack2bf(y0, y1), pack2bf(y2, y3));
