@@ -2390,12 +2390,14 @@ int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 // production 320-row launch: the persistent form for SwiGLU launches of at least 4 tiles per CU (W13: 15 / 5
 // tiles per CU at M = 30720 / 10240, -2.5 / -3 %, C3 +0.8 %; profiles/r3_t320_persistent.txt, r3s2_ab_t320p.txt)
 // unless diag key 10 asks for one tile per workgroup. One tile per workgroup for the blockwise W13 launch
-// (M = 7680: 2 tiles per CU, C5 -0.4 % when persistent), the gated residual (3 / 1 tiles per CU, K = 5888 for
-// W2: no measurable gain) and the head-norm epilogue (its persistent form holds ~45 dwords in scratch across
-// the K loop: +8 % at M = 30720).
+// (M = 7680: 2 tiles per CU, C5 -0.4 % when persistent) and the gated residual (3 / 1 tiles per CU, K = 5888 for
+// W2: no measurable gain). The head-norm epilogue's persistent form (spill-free since round 4: norm weights
+// and RoPE rows read at the use) from 8 tiles per CU: QKVG M = 30720 (12 per CU) 764.6 -> 753.0 us, M = 10240
+// (4 per CU) 258.5 vs 258.7 (profiles/r4_t320_headnorm_persistent.txt).
 int launch_t320(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
-  const int64_t tiles = (int64_t)(a->M / 320) * (a->N / 256);
-  const bool per = ek_of(a) == EK_SWIGLU && !g_gemm_t320_np && tiles >= 4 * (int64_t)cu_count_cached();
+  const int64_t tiles = (int64_t)(a->M / 320) * (a->N / 256), cus = cu_count_cached();
+  const int ek = ek_of(a);
+  const bool per = !g_gemm_t320_np && ((ek == EK_SWIGLU && tiles >= 4 * cus) || (ek == EK_HEADNORM && tiles >= 8 * cus));
   return per ? launch_t320_sp<0, 1>(a, ep, s) : launch_t320_sp<0, 0>(a, ep, s);
 }
 
