@@ -2459,8 +2459,10 @@ constexpr SkCfg kSk[] = {
     {160, 128, 2, 2, 4},  // 10: 144 KB; 11: 156 KB; 12: 144 KB — whole 160-row blocks / wide tiles for the
     {160, 256, 2, 2, 3},  //     weight-streaming launches (QKVG / W13 at 160-640 rows: few, big, K-split
     {128, 256, 2, 2, 3},  //     tiles cut the per-CU re-read of A)
+    {128, 256, 2, 4, 3},  // 13: 144 KB, 8 waves
+    {160, 128, 2, 2, 2},  // 14: 72 KB, two per CU
 };
-constexpr int kNumSk = 12;
+constexpr int kNumSk = 14;
 // `tile` 100 + 10 c + S (c = 1 .. kNumSk, S = 1 .. 9): small-M config c with K split S
 constexpr bool sk_tile(int t) { return t >= 110 && t < 100 + 10 * (kNumSk + 1) && t % 10 != 0; }
 int sk_occ(int c) { return (160 * 1024) / ((kSk[c].bm + kSk[c].bn) * BK * 2 * kSk[c].ns); }
@@ -2607,6 +2609,8 @@ int launch_sk_cfg(const EchoGemmArgs* a, const Epi& ep, int c, int S, void* ws, 
     case 10: return launch_sk<160, 128, 2, 2, 4>(a, ep, S, ws, s);
     case 11: return launch_sk<160, 256, 2, 2, 3>(a, ep, S, ws, s);
     case 12: return launch_sk<128, 256, 2, 2, 3>(a, ep, S, ws, s);
+    case 13: return launch_sk<128, 256, 2, 4, 3>(a, ep, S, ws, s);
+    case 14: return launch_sk<160, 128, 2, 2, 2>(a, ep, S, ws, s);
     default: return ECHO_EINVAL;
   }
 }
