@@ -2517,8 +2517,9 @@ bool sk_plan(const EchoGemmArgs* a, bool allow_split, int* cfg, int* split) {
   //     here                                               K 2048  11.8 8/2 12.5 8/1 15.8 3/1  (r3)
   //                                                        K 5888  17.8 5/4 25.4 6/4 30.2 6/3  58.5 6/1
   //   QKVG + q/k norm + RoPE (N = 8192; round 3: store + head_norm_rope) 22.6 -> 18.9 (5/1),
-  //     37.1 -> 27.0 (1/1), 39.5 -> 33.5 (10/1); W13 SwiGLU at 160 rows 24.4 -> 22.8 (6/1); the other W13 /
-  //     QKVG shapes keep the round-3 pick (as fast or faster there).
+  //     37.1 -> 27.0 (1/1), 39.5 -> 33.5 (10/1); W13 SwiGLU 24.4 -> 22.8 (6/1) at 160 rows, 39.1 -> 35.4 and
+  //     38.1 -> 36.9 (13/1: 128x256 tiles of 8 waves) at 480 / 640; the 1920-row W13 / QKVG keep the round-3
+  //     pick (as fast or faster there).
   const int ek = ek_of(a);
   const bool longk = a->K >= 4096;
   int c, S = 1;
@@ -2530,8 +2531,8 @@ bool sk_plan(const EchoGemmArgs* a, bool allow_split, int* cfg, int* split) {
     else return false;
   } else if (ek == EK_HEADNORM && a->N >= 4096 && Mp <= 768) {
     c = Mp <= 256 ? 5 : Mp <= 512 ? 1 : 10;
-  } else if (ek == EK_SWIGLU && a->N >= 8192 && Mp <= 256) {
-    c = 6;
+  } else if (ek == EK_SWIGLU && a->N >= 8192 && Mp <= 768) {
+    c = Mp <= 256 ? 6 : 13;  // 480 / 640 rows: 39.1 -> 35.4 / 38.1 -> 36.9 us (profiles/r4_sk4_sweep.txt)
   } else {
     return false;
   }
