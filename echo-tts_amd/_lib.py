@@ -71,6 +71,7 @@ SIGNATURES = {
     "echo_gemm_set_diag": (i32, [i32, i32]),
     "echo_gemm_ws_bytes": (i64, [C.POINTER(GemmArgs)]),
     "echo_gemm_ws": (i32, [C.POINTER(GemmArgs), vp, i64, vp]),
+    "echo_attention_set_combine": (i32, [i32]),
     "echo_set_policy_rows": (i32, [i32, i32]),
     "echo_attention": (i32, [C.POINTER(AttnArgs), vp]),
     "echo_attention_variant": (i32, [C.POINTER(AttnArgs), i32, i32, vp, vp]),

@@ -19,12 +19,16 @@
 // conflict-free for both the K row reads and the V transposed reads.
 #include "common.h"
 
+#include <mutex>
 #include <type_traits>
 
 // q / gate row of output row `row` (EchoAttnArgs.q_batch_mod: row groups that share one q copy)
 #define ECHO_QROW(a, row) ((a).q_batch_mod > 0 ? (row) % (a).q_batch_mod : (row))
 
 namespace {
+
+template <class Args>  // EchoAttnArgs, or the split kernel's kernarg-segment view of it
+__device__ void attn_combine_unit(const Args& a, const float* __restrict__ ws, int nsp, int rh, int qi, int c8);
 
 __device__ __forceinline__ int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
@@ -269,7 +273,7 @@ struct SegInfo {
 // stores. Same tile math; only the summation order over keys differs from SP = 0 (fp32-close).
 template <int ABL, int NW, int ST, int KTT = 64, int PS = 0, int SP = 0>
 __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
-    attn_bf16_kernel(EchoAttnArgs a_arg, float* ws, int nsp) {
+    attn_bf16_kernel(EchoAttnArgs a_arg, float* ws, int nsp, int* cnt) {
   static_assert(!PS || (ABL == 0 && ST == 2), "persistent form: production schedule only");
   static_assert(!SP || (ABL == 0 && ST == 2 && !PS), "split-KV form: production schedule only");
   constexpr int QB = 32 * NW;
@@ -290,6 +294,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
   const int nitems = PS ? nqb * kargs->rows * kargs->heads : (int)blockIdx.x + 1;
   (void)ws;
   (void)nsp;
+  (void)cnt;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h2 = lane >> 5, ql = lane & 31;
@@ -641,6 +646,31 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
         }
       }
       (void)inv;
+      if (cnt) {
+        // fused combine: the last of the item's nsp split workgroups to finish merges them. Each workgroup's
+        // partial stores are released at agent scope before it counts itself in on the item's counter; the
+        // last arriver resets the counter for the next launch and acquires before reading the partials
+        // (the counters start at 0: echo_attention_split allocates and clears them once, outside capture)
+        __shared__ int s_last;
+        __threadfence();
+        __syncthreads();
+        if (tid == 0) {
+          int* c = cnt + (row * a.heads + head) * nqb + qb;
+          const int last = __hip_atomic_fetch_add(c, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nsp - 1;
+          if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_last = last;
+        }
+        __syncthreads();
+        if (s_last) {
+          __threadfence();
+          const int rh = row * a.heads + head;
+          // query fastest, as attn_combine_kernel: the partial reads are contiguous over the queries
+          for (int u = tid; u < QB * 16; u += 64 * NW) {
+            const int qq = q0 + u % QB, c8 = u / QB;
+            if (qq < a.n_q) attn_combine_unit(a, ws, nsp, rh, qq, c8);
+          }
+        }
+      }
     } else if constexpr (PS) {
       // (the persistent form keeps the per-lane epilogue: the row form's LDS transposition needs a
       // barrier before the next item's DMA and spills around the item loop — 179 vs 154 us, R = 16)
@@ -1243,12 +1273,11 @@ __global__ void __launch_bounds__(256, 2) attn_pipe_kernel(EchoAttnArgs a) {
 // out = round(round(sum_s w_s O_s / sum_s w_s l_s) * round(sigmoid(gate))) — the roundings of
 // attn_pack_out. 16 queries x 16 column groups per 256-thread block (query fastest: the partial
 // reads are 256-B runs, the 16-B output stores fill whole rows across the block).
-__global__ void __launch_bounds__(256) attn_combine_kernel(EchoAttnArgs a, const float* __restrict__ ws, int nsp) {
-  const int nqb = (a.n_q + 15) / 16;
-  const int qb = blockIdx.x % nqb, rh = blockIdx.x / nqb;  // rh = row * heads + head
+// one (query qi, 8 output columns c8) unit of (row, head) rh: also the fused combine of the split kernel's last
+// workgroup (attn_bf16_kernel, cnt != nullptr), so both forms give the same bits
+template <class Args>
+__device__ void attn_combine_unit(const Args& a, const float* __restrict__ ws, int nsp, int rh, int qi, int c8) {
   const int row = rh / a.heads, head = rh % a.heads;
-  const int qi = qb * 16 + (threadIdx.x & 15), c8 = threadIdx.x >> 4;
-  if (qi >= a.n_q) return;
   const int64_t per_split = (int64_t)a.rows * a.heads * 128 * a.n_q;
   const float* ml = ws + nsp * per_split;
   float mx = -INFINITY;
@@ -1283,6 +1312,14 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(EchoAttnArgs a, const
   }
   *(uint4*)((bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qi * a.o_ld_tok + head * 128 + 8 * c8) =
       make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+}
+
+__global__ void __launch_bounds__(256) attn_combine_kernel(EchoAttnArgs a, const float* __restrict__ ws, int nsp) {
+  const int nqb = (a.n_q + 15) / 16;
+  const int qb = blockIdx.x % nqb, rh = blockIdx.x / nqb;  // rh = row * heads + head
+  const int qi = qb * 16 + (threadIdx.x & 15), c8 = threadIdx.x >> 4;
+  if (qi >= a.n_q) return;
+  attn_combine_unit(a, ws, nsp, rh, qi, c8);
 }
 
 // ----------------------------------------------------------------------------- fp32 (parity mode)
@@ -1407,7 +1444,7 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
   const int qb = (cfg == 1 || cfg == 2 || cfg == 4) ? 256 : 128;
   const dim3 grid(attn_grid(a, qb));
 #define ECHO_ATTN_LAUNCH(A, NW, ST, ...) \
-  hipLaunchKernelGGL((attn_bf16_kernel<A, NW, ST, ##__VA_ARGS__>), grid, dim3(64 * NW), 0, s, *a, (float*)nullptr, 1)
+  hipLaunchKernelGGL((attn_bf16_kernel<A, NW, ST, ##__VA_ARGS__>), grid, dim3(64 * NW), 0, s, *a, (float*)nullptr, 1, (int*)nullptr)
 #define ECHO_ATTN_ABLS(NW, ST)                        \
   switch (abl) {                                      \
     case 0: ECHO_ATTN_LAUNCH(0, NW, ST); break;       \
@@ -1444,13 +1481,13 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       if (abl) return ECHO_EINVAL;
       const int ps_grid = attn_ps_grid(grid.x);
       if (ps_grid <= 0) return ECHO_EINVAL;
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a, (float*)nullptr, 1);
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a, (float*)nullptr, 1, (int*)nullptr);
       break;
     }
     case 6: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 2, 32); break;
     case 9:  // 2 waves x 32 queries per workgroup (production for launches that cannot fill the CUs)
       if (abl) return ECHO_EINVAL;
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 2, 2>), dim3(attn_grid(a, 64)), dim3(128), 0, s, *a, (float*)nullptr, 1);
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 2, 2>), dim3(attn_grid(a, 64)), dim3(128), 0, s, *a, (float*)nullptr, 1, (int*)nullptr);
       break;
     case 7: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 3, 32); break;
     case 10: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(2048, 4, 2); break;  // per-lane epilogue
@@ -1509,7 +1546,7 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
     if (g_attn_pl && !any_causal(a))
       hipLaunchKernelGGL(attn_pl_kernel<0>, dim3(attn_grid(a, 128)), dim3(256), 0, s, *a);
     else
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1);
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1, (int*)nullptr);
   } else {
     hipLaunchKernelGGL(attn_f32_kernel, dim3(attn_grid(a, FQ)), dim3(64), 0, s, *a);
   }
@@ -1521,6 +1558,33 @@ extern int g_policy_num, g_policy_den;  // echo_set_policy_rows (gemm.hip)
 
 namespace {
 int g_attn_split_override = -1;  // echo_attention_set_split: force nsplit (diagnostics), -1 = policy
+int g_attn_fused_combine = 1;    // echo_attention_set_combine: 0 = the separate combine kernel (A/B)
+
+// split-KV item counters of the fused combine: one zeroed array per device, allocated on the first split launch
+// that is not being captured (a graph captured before then keeps the separate combine kernel); each item's last
+// workgroup resets its counter, so the array is all zeros between launches. Concurrent split launches on
+// different streams would share it: they must use the separate combine (echo_attention_set_combine(0)).
+constexpr int kAttnCounters = 1 << 16;
+std::mutex g_cnt_mu;
+int* g_cnt[64] = {};
+
+int* attn_counters(hipStream_t s, int64_t items) {
+  if (!g_attn_fused_combine || items > kAttnCounters) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_cnt_mu);
+  if (g_cnt[dev]) return g_cnt[dev];
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  int* p = nullptr;
+  if (hipMalloc(&p, kAttnCounters * sizeof(int)) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, kAttnCounters * sizeof(int)) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  g_cnt[dev] = p;
+  return p;
+}
 
 int cu_count() {
   static int cus = 0;
@@ -1569,6 +1633,12 @@ extern "C" int echo_attention_set_pipeline(int32_t on) {
   return 0;
 }
 
+extern "C" int echo_attention_set_combine(int32_t fused) {
+  if (fused < 0 || fused > 1) return ECHO_EINVAL;
+  g_attn_fused_combine = fused;
+  return 0;
+}
+
 extern "C" int echo_attention_set_split(int32_t nsplit) {
   if (nsplit < -1 || nsplit > 16) return ECHO_EINVAL;
   g_attn_split_override = nsplit;
@@ -1583,9 +1653,11 @@ extern "C" int echo_attention_split(const EchoAttnArgs* a, int32_t nsplit, void*
   if (nsplit > 16) return ECHO_EINVAL;
   if (!ws || (uintptr_t)ws % 16 || ws_bytes < echo_attention_split_ws_bytes(a, nsplit)) return ECHO_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  int* cnt = attn_counters(s, attn_grid(a, 128));
   hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 0, 1>), dim3(attn_grid(a, 128) * nsplit), dim3(256), 0, s, *a,
-                     (float*)ws, (int)nsplit);
+                     (float*)ws, (int)nsplit, cnt);
   ECHO_LAUNCH_CHECK();
+  if (cnt) return 0;  // merged by each item's last workgroup
   hipLaunchKernelGGL(attn_combine_kernel, dim3(a->rows * a->heads * ((a->n_q + 15) / 16)), dim3(256), 0, s, *a,
                      (const float*)ws, (int)nsplit);
   ECHO_LAUNCH_CHECK();

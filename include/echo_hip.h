@@ -161,7 +161,8 @@ int echo_attention(const EchoAttnArgs* args, void* stream);
 /* Split-KV form of echo_attention for launches that leave most CUs idle (B = 1 sampler steps,
  * blockwise blocks): each (128-query block, row, head) item's key tiles are split over `nsplit`
  * workgroups that store unnormalised partials (O fp32, running max, row sum) into `ws`, and a
- * combine pass merges them, normalises, gates and stores `out` (same roundings as echo_attention;
+ * combine step (each item's last workgroup, or a separate pass: echo_attention_set_combine) merges
+ * them, normalises, gates and stores `out` (same roundings as echo_attention;
  * only the fp32 summation order over keys differs). nsplit <= 1 runs echo_attention.
  * `ws`: device, 16-B aligned, >= echo_attention_split_ws_bytes(args, nsplit) bytes.
  * Replaces the same reference lines as echo_attention (model.py:237-264, 144-157). */
@@ -169,6 +170,12 @@ int echo_attention_split(const EchoAttnArgs* args, int32_t nsplit, void* ws, int
 int64_t echo_attention_split_ws_bytes(const EchoAttnArgs* args, int32_t nsplit);
 /* Host policy: the split count echo_attention_split should use for these shapes (1 = none). */
 int32_t echo_attention_pick_split(const EchoAttnArgs* args);
+/* Split-KV launches merge their splits in the split kernel itself: the last workgroup of each (row, head,
+ * query block) to finish combines the partials (an agent-scope counter per item in a per-device array the
+ * library allocates and clears on the first split launch outside stream capture). 0 = the separate combine
+ * kernel (also what a launch gets when that first launch happens under capture); bitwise the same. Concurrent
+ * split launches on different streams of one device must use 0. */
+int echo_attention_set_combine(int32_t fused);
 /* Diagnostics: force the policy's answer (0/1 = never split, 2..16), -1 = back to the policy. */
 int echo_attention_set_split(int32_t nsplit);
 /* Diagnostics: 1 (default) = non-causal bf16 launches run the asm-owned software-pipelined kernel

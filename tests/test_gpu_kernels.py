@@ -438,6 +438,37 @@ def test_attention_split_kv(nsplit, R, n_q):
     split_close(got, ref, ref_attention(qkvg[:, :, 0], segs, qkvg[:, :, 3], 128 ** -0.5, BF))
 
 
+@pytest.mark.parametrize("nsplit", [2, 3, 4, 16])
+@pytest.mark.parametrize("R,n_q", [(1, 640), (3, 160), (1, 37)])
+def test_attention_split_fused_combine_bitwise(nsplit, R, n_q):
+    """The split kernel's fused combine (each item's last workgroup merges the partials, agent-scope counters
+    that reset themselves) is bitwise the separate combine kernel — eager, repeated (counters back at 0
+    after every launch) and replayed from a captured hipGraph."""
+    qkvg, segs = _small_batch_segments(1, R, n_q, H=4, tl_valid=271)
+    ref = torch.full((R, n_q, 4, 128), float("nan"), device=DEV, dtype=BF)
+    with ops.attention_split(nsplit), ops.attention_combine(False):
+        ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
+    got = torch.full_like(ref, float("nan"))
+    with ops.attention_split(nsplit):
+        for _ in range(3):
+            got.fill_(float("nan"))
+            ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
+            torch.cuda.synchronize()
+            assert torch.equal(got, ref)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
+        torch.cuda.current_stream().wait_stream(s)
+        for _ in range(3):
+            got.fill_(float("nan"))
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(got, ref)
+
+
 @pytest.mark.parametrize("L_", [37, 160, 333])
 def test_attention_split_kv_causal(L_):
     """Split-KV on a causal (encoder) segment: queries whose split holds no visible key."""
