@@ -1558,7 +1558,11 @@ extern int g_policy_num, g_policy_den;  // echo_set_policy_rows (gemm.hip)
 
 namespace {
 int g_attn_split_override = -1;  // echo_attention_set_split: force nsplit (diagnostics), -1 = policy
-int g_attn_fused_combine = 1;    // echo_attention_set_combine: 0 = the separate combine kernel (A/B)
+// echo_attention_set_combine: 1 = each item's last split workgroup merges the partials. Measured slower on
+// MI355X (C2 136.2 -> 124.8, C5 at B = 1 66.8 -> 50.4 audio-s/s, profiles/r4_attn_fused_combine.txt): the
+// agent-scope release each split workgroup needs writes back its XCD's L2 (buffer_wbl2), and the merge runs
+// on one CU per item. Default 0: the separate combine kernel.
+int g_attn_fused_combine = 0;
 
 // split-KV item counters of the fused combine: one zeroed array per device, allocated on the first split launch
 // that is not being captured (a graph captured before then keeps the separate combine kernel); each item's last

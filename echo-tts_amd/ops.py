@@ -204,15 +204,15 @@ def current_policy_rows() -> Tuple[int, int]:
 
 @contextlib.contextmanager
 def attention_combine(fused: bool):
-    """Split-KV launches merge their splits in each item's last workgroup (True, the default) or in the
-    separate combine kernel (False) inside the block (A/B tests; bitwise the same)."""
+    """Split-KV launches merge their splits in each item's last workgroup (True) or in the separate combine
+    kernel (False, the default: faster on MI355X) inside the block (A/B tests; bitwise the same)."""
     rc = lib().echo_attention_set_combine(int(bool(fused)))
     if rc:
         raise RuntimeError(f"echo_attention_set_combine({fused}) failed: {rc}")
     try:
         yield
     finally:
-        lib().echo_attention_set_combine(1)
+        lib().echo_attention_set_combine(0)
 
 
 @contextlib.contextmanager

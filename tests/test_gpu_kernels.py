@@ -449,7 +449,7 @@ def test_attention_split_fused_combine_bitwise(nsplit, R, n_q):
     with ops.attention_split(nsplit), ops.attention_combine(False):
         ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
     got = torch.full_like(ref, float("nan"))
-    with ops.attention_split(nsplit):
+    with ops.attention_split(nsplit), ops.attention_combine(True):
         for _ in range(3):
             got.fill_(float("nan"))
             ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
