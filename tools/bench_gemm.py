@@ -87,8 +87,11 @@ def main():
     tiles = [int(t) for t in args.tiles.split(",")]
     if args.sk:
         cs, ss = args.sk.split("x")
-        c0, c1 = (int(v) for v in cs.split("-")) if "-" in cs else (int(cs), int(cs))
-        tiles += [100 + 10 * c + int(sv) for c in range(c0, c1 + 1) for sv in ss.split(",")]
+        cfgs = []
+        for part in cs.split(","):  # "1-6" or "1,3,5" or a mix
+            c0, c1 = (int(v) for v in part.split("-")) if "-" in part else (int(part), int(part))
+            cfgs += range(c0, c1 + 1)
+        tiles += [100 + 10 * c + int(sv) for c in cfgs for sv in ss.split(",")]
     dev = "cuda"
     torch.manual_seed(0)
     for name, M, N, K, epi in shapes:
