@@ -523,8 +523,12 @@ gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __r
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int STAGE = (BM + BN) * BK;  // elements per ring slot
-  constexpr int DOPS = (BM + BN) * 8 / NT;  // LDS-DMA wave-instructions per slot
-  static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "staging split");
+  // LDS-DMA wave-instructions per slot: 8 rows each; where the rows do not split evenly over the waves the
+  // last round wraps to rows already staged (a duplicate DMA of the same bytes to the same LDS address), so
+  // every wave issues the same count and the counted waits stay uniform
+  constexpr int AI = (BM * 8 + NT - 1) / NT, BI = (BN * 8 + NT - 1) / NT;
+  constexpr int DOPS = AI + BI;
+  static_assert(BM % 8 == 0 && BN % 8 == 0, "8-row DMA groups");
   static_assert(NS >= 2 && NS <= 5 && DOPS * (NS - 2) <= 63, "ring depth / vmcnt range");
   __shared__ __attribute__((aligned(16))) bf16_t lds[NS * STAGE];
 
@@ -562,16 +566,16 @@ gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __r
     const bf16_t* wbase = W + k0;
     bf16_t* dst = lds + slot * STAGE;
 #pragma unroll
-    for (int i = 0; i < BM * 8 / NT; ++i) {
-      const int rb = (i * NW + wid) * 8;
+    for (int i = 0; i < AI; ++i) {
+      const int rb = ((i * NW + wid) * 8) % BM;
       const int row = rb + (lane >> 3);
       const int gc = (lane & 7) ^ ((row >> 1) & 7);
       const uint32_t off = (uint32_t)(((int64_t)min(m0 + row, M - 1) * lda + gc * 8) * 2);
       glds16s(abase, off, __builtin_amdgcn_readfirstlane(lds_addr_of(dst + rb * BK)));
     }
 #pragma unroll
-    for (int i = 0; i < BN * 8 / NT; ++i) {
-      const int rb = (i * NW + wid) * 8;
+    for (int i = 0; i < BI; ++i) {
+      const int rb = ((i * NW + wid) * 8) % BN;
       const int row = rb + (lane >> 3);
       const int gc = (lane & 7) ^ ((row >> 1) & 7);
       const uint32_t off = (uint32_t)(((int64_t)min(n0 + row, N - 1) * ldw + gc * 8) * 2);
@@ -2461,8 +2465,10 @@ constexpr SkCfg kSk[] = {
     {128, 256, 2, 2, 3},  //     tiles cut the per-CU re-read of A)
     {128, 256, 2, 4, 3},  // 13: 144 KB, 8 waves
     {160, 128, 2, 2, 2},  // 14: 72 KB, two per CU
+    {160, 128, 2, 4, 4},  // 15: 144 KB, 8 waves (160-row blocks: one round at M = 2560, three at 7680, N = 2048)
+    {160, 128, 2, 4, 3},  // 16: 108 KB
 };
-constexpr int kNumSk = 14;
+constexpr int kNumSk = 16;
 // `tile` 100 + 10 c + S (c = 1 .. kNumSk, S = 1 .. 9): small-M config c with K split S
 constexpr bool sk_tile(int t) { return t >= 110 && t < 100 + 10 * (kNumSk + 1) && t % 10 != 0; }
 int sk_occ(int c) { return (160 * 1024) / ((kSk[c].bm + kSk[c].bn) * BK * 2 * kSk[c].ns); }
@@ -2612,6 +2618,8 @@ int launch_sk_cfg(const EchoGemmArgs* a, const Epi& ep, int c, int S, void* ws, 
     case 12: return launch_sk<128, 256, 2, 2, 3>(a, ep, S, ws, s);
     case 13: return launch_sk<128, 256, 2, 4, 3>(a, ep, S, ws, s);
     case 14: return launch_sk<160, 128, 2, 2, 2>(a, ep, S, ws, s);
+    case 15: return launch_sk<160, 128, 2, 4, 4>(a, ep, S, ws, s);
+    case 16: return launch_sk<160, 128, 2, 4, 3>(a, ep, S, ws, s);
     default: return ECHO_EINVAL;
   }
 }

@@ -127,7 +127,7 @@ int echo_set_policy_rows(int32_t num, int32_t den);
  * force either form for any epilogue) (A/B timing, tools/bench_streams.py --diag; all bitwise-equal).
  * key 11: 1 = never split K in echo_gemm_ws (the B = 1 runs that tests compare bitwise with B = 16 rows);
  * key 12: 1 = no small-M kernel in the auto pick (the round-3 small tiles; A/B).
- * `tile` 100 + 10*C + S (C = small-M config 1..14, S = split 1..9) forces a small-M launch (tools/bench_gemm.py). */
+ * `tile` 100 + 10*C + S (C = small-M config 1..16, S = split 1..9) forces a small-M launch (tools/bench_gemm.py). */
 int echo_gemm_set_diag(int32_t key, int32_t value);
 
 /* One key/value segment of the joint attention (model.py:246-253): rows of

@@ -856,7 +856,7 @@ def test_gemm_headnorm_t320(M, H, pos0, rh, K):
         assert torch.equal(got, ref), tile
 
 
-SK_CFGS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14)
+SK_CFGS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16)
 
 
 def _sk_case(M, N, K, epi, seed=0):
