@@ -2534,6 +2534,9 @@ bool sk_plan(const EchoGemmArgs* a, bool allow_split, int* cfg, int* split) {
     else if (Mp <= 512) { c = longk ? 6 : 8; S = longk ? 4 : 1; }
     else if (Mp <= 768) { c = longk ? 6 : 3; S = longk ? 3 : 1; }
     else if (Mp <= 2048 && longk) c = 6;
+    // the blockwise B = 16 plain step (M = 2560: 256 tiles of 160x128 = one round): 37.9 -> 31.3 us (Wo),
+    // 85.6 -> 73.3 (W2) (profiles/r4_sk5_sweep.txt; hipBLASLt's plain store 26.7 / 58.5)
+    else if (Mp > 2048 && Mp <= 3072) c = 15;
     else return false;
   } else if (ek == EK_HEADNORM && a->N >= 4096 && Mp <= 768) {
     c = Mp <= 256 ? 5 : Mp <= 512 ? 1 : 10;
