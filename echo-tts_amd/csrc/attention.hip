@@ -761,9 +761,13 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
 // K second, both younger than every piece the wait needs) and each tile's loads get two tiles of latency
 // budget instead of one (NK = NV = 2 waits vmcnt(0) for the loads it issued at its own top). LDS: (NK + NV) x
 // 16 KiB — 2 + 2 and 3 + 2 keep two workgroups per CU, 3 + 3 and 4 + 4 one.
-template <int ABL, int NW = 4, int NK = 2, int NV = 2>
+// SP = 1: the split-KV form (attn_bf16_kernel's SP = 1 layout: split s of nsp walks tiles [s n / nsp, (s+1) n / nsp)
+// of the item's flat tile list and stores its unnormalised partial to `ws` for attn_combine_kernel): bitwise the
+// compiler-scheduled split kernel's partials, with this kernel's pipelined tile loop.
+template <int ABL, int NW = 4, int NK = 2, int NV = 2, int SP = 0>
 __global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __attribute__((amdgpu_num_vgpr(96)))
-    attn_pl_kernel(EchoAttnArgs a_arg) {
+    attn_pl_kernel(EchoAttnArgs a_arg, float* ws, int nsp) {
+  static_assert(!SP || (ABL == 0 && NW == 4 && NK == 2 && NV == 2), "split-KV form: production schedule only");
   constexpr int QB = 32 * NW, DPT = 16 / NW, KTT = KT;
   static_assert(NK >= 2 && NV >= 2 && NK <= 4 && NV <= 4, "ring slots (attn_pl.inc MAX_SLOTS)");
   static_assert(!(ABL & 128) || (NK == 2 && NV == 2), "ablation 128 is defined on the 2 + 2 ring");
@@ -778,7 +782,9 @@ __global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __a
   const int nqb = (a.n_q + QB - 1) / QB;
   const int L = remap_xcd(blockIdx.x, gridDim.x);
   const int qb = L % nqb;
-  const int Lr = L / nqb;  // rows fastest (see attn_bf16_kernel)
+  const int Lr = SP ? L / (nqb * nsp) : L / nqb;  // rows fastest (see attn_bf16_kernel)
+  const int sp = SP ? (L / nqb) % nsp : 0;
+  (void)ws;
   int row = Lr % a.rows;
   if constexpr ((ABL & 32) != 0) {
     const int B = a.nseg > 1 ? a.seg[1].batch_mod : a.rows;
@@ -812,6 +818,12 @@ __global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __a
   Cursor kc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // K DMA (NK - 1 tiles ahead of the QK)
   Cursor vc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // V DMA (NV - 1 tiles ahead of the PV)
   Cursor mc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // the tile whose scores are masked / maxed
+  if constexpr (SP) {
+    // this split's tile range of the flat list (scalar cursor walk; <= ~20 tiles)
+    const int tb = sp * ntiles / nsp, te = (sp + 1) * ntiles / nsp;
+    for (int i = 0; i < tb; ++i) { advance(kc); advance(vc); advance(mc); }
+    ntiles = te - tb;
+  }
 
   const int dr = lane >> 4, dp = lane & 15;
   // one tile's share of this wave (DPT pieces) into slot `slot` of the K (part 0) or V (part 1) ring
@@ -977,6 +989,33 @@ __global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __a
   const float lt = halves_sum(l_run);
   const float inv = 1.0f / lt;
   const int nv = a.n_q - (q0 + w * 32);  // wave-uniform
+  if constexpr (SP) {
+    // unnormalised partial, attn_bf16_kernel's SP layout: chunk c = d / 4 of query qi at ws[it][c][qi], then
+    // (m in exp2 units, l) per query after all splits' O
+    const int qi = q0 + w * 32 + ql;
+    if (qi < a.n_q) {
+      const int64_t it = ((int64_t)sp * a.rows + row) * a.heads + head;
+      float* wo = ws + it * 128 * a.n_q;
+      float od[16];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        if (dt == 0) pl_get_o_0(od); else if (dt == 1) pl_get_o_1(od); else if (dt == 2) pl_get_o_2(od); else pl_get_o_3(od);
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          const int c = dt * 8 + 2 * rg + h2;
+          *(float4*)(wo + ((int64_t)c * a.n_q + qi) * 4) =
+              make_float4(od[4 * rg], od[4 * rg + 1], od[4 * rg + 2], od[4 * rg + 3]);
+        }
+      }
+      if (h2 == 0) {
+        float* wml = ws + (int64_t)nsp * a.rows * a.heads * 128 * a.n_q + (it * a.n_q + qi) * 2;
+        *(float2*)wml = make_float2(m_run == -INFINITY ? -INFINITY : m_run * sl2, lt);
+      }
+    }
+    (void)inv;
+    (void)nv;
+    return;
+  }
   if (nv > 0) {
     uint4 v4[8];
     auto pack_dt = [&](const float (&od)[16], int dt) __attribute__((always_inline)) {
@@ -1493,30 +1532,30 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 10: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(2048, 4, 2); break;  // per-lane epilogue
     case 11:  // asm-owned software pipeline (production for non-causal launches)
       if (abl || any_causal(a)) return ECHO_EINVAL;
-      hipLaunchKernelGGL(attn_pl_kernel<0>, grid, dim3(256), 0, s, *a);
+      hipLaunchKernelGGL(attn_pl_kernel<0>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1);
       break;
-    case 12: hipLaunchKernelGGL(attn_pl_kernel<1>, grid, dim3(256), 0, s, *a); break;
-    case 13: hipLaunchKernelGGL(attn_pl_kernel<2>, grid, dim3(256), 0, s, *a); break;
-    case 14: hipLaunchKernelGGL(attn_pl_kernel<4>, grid, dim3(256), 0, s, *a); break;
-    case 15: hipLaunchKernelGGL(attn_pl_kernel<8>, grid, dim3(256), 0, s, *a); break;
-    case 16: hipLaunchKernelGGL(attn_pl_kernel<16>, grid, dim3(256), 0, s, *a); break;
-    case 17: hipLaunchKernelGGL(attn_pl_kernel<6>, grid, dim3(256), 0, s, *a); break;
-    case 18: hipLaunchKernelGGL(attn_pl_kernel<7>, grid, dim3(256), 0, s, *a); break;
-    case 19: hipLaunchKernelGGL(attn_pl_kernel<32>, grid, dim3(256), 0, s, *a); break;
-    case 25: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<128>, grid, dim3(256), 0, s, *a); break;
-    case 23: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<64>, grid, dim3(256), 0, s, *a); break;
-    case 24: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<32>, grid, dim3(256), 0, s, *a); break;
+    case 12: hipLaunchKernelGGL(attn_pl_kernel<1>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 13: hipLaunchKernelGGL(attn_pl_kernel<2>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 14: hipLaunchKernelGGL(attn_pl_kernel<4>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 15: hipLaunchKernelGGL(attn_pl_kernel<8>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 16: hipLaunchKernelGGL(attn_pl_kernel<16>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 17: hipLaunchKernelGGL(attn_pl_kernel<6>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 18: hipLaunchKernelGGL(attn_pl_kernel<7>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 19: hipLaunchKernelGGL(attn_pl_kernel<32>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 25: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<128>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 23: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<64>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 24: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<32>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
     // asm pipeline with deeper K / V rings (NK + NV slots of 16 KiB; counted waits keep each tile's DMA in
     // flight across its barrier): 26 = 3 + 2 (80 KiB, two workgroups per CU), 27 = 3 + 3, 28 = 4 + 4 (one per CU)
-    case 26: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 3, 2>), grid, dim3(256), 0, s, *a); break;
-    case 27: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 3, 3>), grid, dim3(256), 0, s, *a); break;
-    case 28: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 4, 4>), grid, dim3(256), 0, s, *a); break;
+    case 26: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 3, 2>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 27: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 3, 3>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 28: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 4, 4>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
     case 20: case 21: case 22: {  // asm pipeline at 8 waves x 32 queries (21: no tile loop, 22: no X / Y bodies)
       if (any_causal(a)) return ECHO_EINVAL;
       const dim3 g8(attn_grid(a, 256));
-      if (cfg == 20) hipLaunchKernelGGL((attn_pl_kernel<0, 8>), g8, dim3(512), 0, s, *a);
-      else if (cfg == 21) hipLaunchKernelGGL((attn_pl_kernel<16, 8>), g8, dim3(512), 0, s, *a);
-      else hipLaunchKernelGGL((attn_pl_kernel<6, 8>), g8, dim3(512), 0, s, *a);
+      if (cfg == 20) hipLaunchKernelGGL((attn_pl_kernel<0, 8>), g8, dim3(512), 0, s, *a, (float*)nullptr, 1);
+      else if (cfg == 21) hipLaunchKernelGGL((attn_pl_kernel<16, 8>), g8, dim3(512), 0, s, *a, (float*)nullptr, 1);
+      else hipLaunchKernelGGL((attn_pl_kernel<6, 8>), g8, dim3(512), 0, s, *a, (float*)nullptr, 1);
       break;
     }
     default: return ECHO_EINVAL;
@@ -1544,7 +1583,7 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
     // non-causal launches (every decoder attention) run the asm-owned pipeline (attn_pl_kernel, bitwise
     // equal to attn_bf16_kernel<0, 4, 2>); causal ones (speaker / latent encoders) the compiler-scheduled kernel
     if (g_attn_pl && !any_causal(a))
-      hipLaunchKernelGGL(attn_pl_kernel<0>, dim3(attn_grid(a, 128)), dim3(256), 0, s, *a);
+      hipLaunchKernelGGL(attn_pl_kernel<0>, dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1);
     else
       hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1, (int*)nullptr);
   } else {
@@ -1563,6 +1602,7 @@ int g_attn_split_override = -1;  // echo_attention_set_split: force nsplit (diag
 // agent-scope release each split workgroup needs writes back its XCD's L2 (buffer_wbl2), and the merge runs
 // on one CU per item. Default 0: the separate combine kernel.
 int g_attn_fused_combine = 0;
+int g_attn_split_pl = 1;  // echo_attention_set_combine(2 / 3): split kernel = pipelined (1) or compiler-scheduled (0)
 
 // split-KV item counters of the fused combine: one zeroed array per device, allocated on the first split launch
 // that is not being captured (a graph captured before then keeps the separate combine kernel); each item's last
@@ -1638,8 +1678,9 @@ extern "C" int echo_attention_set_pipeline(int32_t on) {
 }
 
 extern "C" int echo_attention_set_combine(int32_t fused) {
-  if (fused < 0 || fused > 1) return ECHO_EINVAL;
-  g_attn_fused_combine = fused;
+  if (fused < 0 || fused > 3) return ECHO_EINVAL;
+  if (fused >= 2) g_attn_split_pl = fused == 3;  // diagnostics: 2 = compiler-scheduled split kernel, 3 = pipelined
+  else g_attn_fused_combine = fused;
   return 0;
 }
 
@@ -1658,8 +1699,12 @@ extern "C" int echo_attention_split(const EchoAttnArgs* a, int32_t nsplit, void*
   if (!ws || (uintptr_t)ws % 16 || ws_bytes < echo_attention_split_ws_bytes(a, nsplit)) return ECHO_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   int* cnt = attn_counters(s, attn_grid(a, 128));
-  hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 0, 1>), dim3(attn_grid(a, 128) * nsplit), dim3(256), 0, s, *a,
-                     (float*)ws, (int)nsplit, cnt);
+  if (g_attn_pl && !cnt && !any_causal(a) && g_attn_split_pl)  // the pipelined split kernel (bitwise the same partials)
+    hipLaunchKernelGGL((attn_pl_kernel<0, 4, 2, 2, 1>), dim3(attn_grid(a, 128) * nsplit), dim3(256), 0, s, *a,
+                       (float*)ws, (int)nsplit);
+  else
+    hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 0, 1>), dim3(attn_grid(a, 128) * nsplit), dim3(256), 0, s, *a,
+                       (float*)ws, (int)nsplit, cnt);
   ECHO_LAUNCH_CHECK();
   if (cnt) return 0;  // merged by each item's last workgroup
   hipLaunchKernelGGL(attn_combine_kernel, dim3(a->rows * a->heads * ((a->n_q + 15) / 16)), dim3(256), 0, s, *a,

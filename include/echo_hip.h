@@ -174,7 +174,8 @@ int32_t echo_attention_pick_split(const EchoAttnArgs* args);
  * query block) to finish combines the partials (an agent-scope counter per item in a per-device array the
  * library allocates and clears on the first split launch outside stream capture; a launch before that, under
  * capture, uses the combine kernel); bitwise the same. Concurrent split launches on different streams of one
- * device must not use it. 0 (default): the separate combine kernel — measured faster on MI355X. */
+ * device must not use it. 0 (default): the separate combine kernel — measured faster on MI355X.
+ * Diagnostics: 2 / 3 = the split kernel on the compiler-scheduled / asm-pipelined (default) tile loop. */
 int echo_attention_set_combine(int32_t fused);
 /* Diagnostics: force the policy's answer (0/1 = never split, 2..16), -1 = back to the policy. */
 int echo_attention_set_split(int32_t nsplit);

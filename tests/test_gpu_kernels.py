@@ -469,6 +469,29 @@ def test_attention_split_fused_combine_bitwise(nsplit, R, n_q):
             assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("nsplit", [2, 3, 4, 16])
+@pytest.mark.parametrize("R,n_q", [(1, 640), (3, 160), (1, 37)])
+def test_attention_split_pipelined_bitwise(nsplit, R, n_q):
+    """The split kernel on the asm-pipelined tile loop (attn_pl_kernel SP = 1, production) stores bitwise the
+    partials of the compiler-scheduled split kernel (attn_bf16_kernel SP = 1): equal outputs after the
+    combine, incl. splits with no tiles."""
+    lib = L.load()
+    qkvg, segs = _small_batch_segments(1, R, n_q, H=4, tl_valid=271)
+    ref = torch.full((R, n_q, 4, 128), float("nan"), device=DEV, dtype=BF)
+    got = torch.full_like(ref, float("nan"))
+    try:
+        assert lib.echo_attention_set_combine(2) == 0
+        with ops.attention_split(nsplit):
+            ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
+        assert lib.echo_attention_set_combine(3) == 0
+        with ops.attention_split(nsplit):
+            ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
+    finally:
+        lib.echo_attention_set_combine(3)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
 @pytest.mark.parametrize("L_", [37, 160, 333])
 def test_attention_split_kv_causal(L_):
     """Split-KV on a causal (encoder) segment: queries whose split holds no visible key."""
