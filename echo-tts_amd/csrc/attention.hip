@@ -933,6 +933,10 @@ __global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __a
       if (t + 2 < ntiles && !(ABL & 1)) dma_part(kc, 0, P);      // K(t+2) -> K slot t & 1 (K(t) was read in X(t-1))
       // V(t+1) -> V slot (t+1) & 1 (V(t-1) was read in Y(t-1)); ABL 128: issued between X(t) and Y(t) instead
       if (!(ABL & 128) && t + 1 < ntiles && !(ABL & 1)) dma_part(vc, 1, 1 - P);
+    } else if constexpr (NK == 2) {
+      // K(t+2) first (waited at this tile's end), then V(t+NV-1), which stays in flight across the barrier
+      if (t + NK < ntiles && !(ABL & 1)) dma_part(kc, 0, U % NK);
+      if (t + NV - 1 < ntiles && !(ABL & 1)) { dma_part(vc, 1, (U + NV - 1) % NV); ++issued; }
     } else {
       if (t + NV - 1 < ntiles && !(ABL & 1)) { dma_part(vc, 1, (U + NV - 1) % NV); ++issued; }  // V first
       if (t + NK < ntiles && !(ABL & 1)) { dma_part(kc, 0, U % NK); ++issued; }
@@ -959,8 +963,9 @@ __global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __a
     if constexpr (!(ABL & 8)) {
       // K(t+2) and V(t+1) must have landed (every wave's share, then the barrier); with NK, NV >= 3 the tiles
       // issued at this tile's top are younger than both and stay in flight (NV == 2: V(t+1) is this tile's V
-      // issue, so only the K issued after it may stay; NK == 2: K(t+2) is this tile's K issue, the youngest)
-      const int keep = (NK == 2 && NV == 2) ? 0 : NK == 2 ? 0 : NV == 2 ? (issued == 2 ? 1 : 0) : issued;
+      // issue, so only the K issued after it may stay; NK == 2, NV >= 3: K(t+2) is issued first, V(t+NV-1)
+      // after it stays in flight)
+      const int keep = (NK == 2 && NV == 2) ? 0 : NK == 2 ? issued : NV == 2 ? (issued == 2 ? 1 : 0) : issued;
       if (keep == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
       else if (keep == 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(DPT) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * DPT) : "memory");
@@ -1550,6 +1555,7 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 26: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 3, 2>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
     case 27: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 3, 3>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
     case 28: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 4, 4>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 29: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 2, 3>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
     case 20: case 21: case 22: {  // asm pipeline at 8 waves x 32 queries (21: no tile loop, 22: no X / Y bodies)
       if (any_causal(a)) return ECHO_EINVAL;
       const dim3 g8(attn_grid(a, 256));

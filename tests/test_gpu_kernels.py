@@ -596,9 +596,9 @@ def test_attention_pipeline_bitwise(case):
         got.fill_(float("nan"))
         ops.attention(q[:, :, 0], segs, out=got, gate=gate)
     assert torch.equal(got, ref)
-    # deeper K / V rings (variants 26 / 27 / 28: 3 + 2, 3 + 3, 4 + 4 slots, counted waits across the barrier):
-    # the same bodies on other LDS slots, bitwise equal
-    for v in (26, 27, 28):
+    # deeper K / V rings (variants 26 / 27 / 28 / 29: 3 + 2, 3 + 3, 4 + 4, 2 + 3 slots, counted waits across the
+    # barrier): the same bodies on other LDS slots, bitwise equal
+    for v in (26, 27, 28, 29):
         got.fill_(float("nan"))
         ops.attention_variant(q[:, :, 0], segs, out=got, gate=gate, variant=v)
         torch.cuda.synchronize()
