@@ -1608,7 +1608,10 @@ int g_attn_split_override = -1;  // echo_attention_set_split: force nsplit (diag
 // agent-scope release each split workgroup needs writes back its XCD's L2 (buffer_wbl2), and the merge runs
 // on one CU per item. Default 0: the separate combine kernel.
 int g_attn_fused_combine = 0;
-int g_attn_split_pl = 1;  // echo_attention_set_combine(2 / 3): split kernel = pipelined (1) or compiler-scheduled (0)
+// echo_attention_set_combine(2 / 3): the split kernel on the compiler-scheduled (0, default) or asm-pipelined (1)
+// tile loop — bitwise the same partials; at the B = 1 policy splits the compiler-scheduled one is 2-4 % faster
+// (one workgroup per CU: 29.0 vs 29.7, 24.6 vs 25.0, 20.5 vs 21.3 us; profiles/r4_attn_split_kernels.txt)
+int g_attn_split_pl = 0;
 
 // split-KV item counters of the fused combine: one zeroed array per device, allocated on the first split launch
 // that is not being captured (a graph captured before then keeps the separate combine kernel); each item's last

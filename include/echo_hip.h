@@ -175,7 +175,7 @@ int32_t echo_attention_pick_split(const EchoAttnArgs* args);
  * library allocates and clears on the first split launch outside stream capture; a launch before that, under
  * capture, uses the combine kernel); bitwise the same. Concurrent split launches on different streams of one
  * device must not use it. 0 (default): the separate combine kernel — measured faster on MI355X.
- * Diagnostics: 2 / 3 = the split kernel on the compiler-scheduled / asm-pipelined (default) tile loop. */
+ * Diagnostics: 2 / 3 = the split kernel on the compiler-scheduled (default) / asm-pipelined tile loop. */
 int echo_attention_set_combine(int32_t fused);
 /* Diagnostics: force the policy's answer (0/1 = never split, 2..16), -1 = back to the policy. */
 int echo_attention_set_split(int32_t nsplit);

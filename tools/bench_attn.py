@@ -92,7 +92,7 @@ def main():
                             with ops.attention_split(c):
                                 f()
                                 tm[(c, kn)].append(timeit(f, rounds=1))
-                ops.lib().echo_attention_set_combine(3)
+                ops.lib().echo_attention_set_combine(2)
                 ops.lib().echo_attention_set_split(-1)
                 line = "  ".join(f"s{c}{kn} {sorted(v)[3] * 1e3:7.1f}" for (c, kn), v in tm.items())
                 print(f"R={R:3d} {name:10s} us by split: {line}", flush=True)
