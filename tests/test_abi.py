@@ -207,3 +207,38 @@ def test_attention_split_host_policy(lib):
     finally:
         assert lib.echo_attention_set_split(-1) == 0
     assert lib.echo_attention_set_split(17) != 0
+
+
+def test_gemm_small_m_plan_host_policy(lib):
+    """The small-M plan (gemm.hip sk_plan, host-only) through echo_gemm_ws_bytes: which launches split K and
+    how much fp32 slab space they need (S x M x N x 4), the direct (unsplit) shapes needing none, and the
+    world-size-invariant policy rows (echo_set_policy_rows): a rank holding 1 of 8 prompts plans as the
+    8-prompt launch would. Also the fused residual + AdaLN and split-kernel knobs' argument checks."""
+    fake = 1 << 20  # 16-B aligned, never dereferenced by the host plan
+
+    def args(M, N, K, epi):
+        g = L.GemmArgs()
+        g.dtype, g.M, g.N, g.K, g.batch = 0, M, N, K, 1
+        g.A = g.W = g.C = g.aux = fake
+        g.lda, g.ldw, g.ldc, g.ld_aux = K, K, N, N
+        g.epilogue = epi
+        return g
+
+    ws = lambda M, N, K, epi=L.EPI_RESID: lib.echo_gemm_ws_bytes(C.byref(args(M, N, K, epi)))  # noqa: E731
+    assert ws(160, 2048, 5888) == 4 * 160 * 2048 * 4     # W2, one 160-latent block: config 5, 4 K splits
+    assert ws(480, 2048, 5888) == 4 * 480 * 2048 * 4     # CFG rows of a block: config 6, 4 splits
+    assert ws(640, 2048, 5888) == 3 * 640 * 2048 * 4     # C2 plain step
+    assert ws(160, 2048, 2048) == 2 * 160 * 2048 * 4     # Wo at 160 rows: 2 splits
+    assert ws(480, 2048, 2048) == 0                      # direct epilogue, no split
+    assert ws(1920, 2048, 5888) == 0                     # C2 CFG W2: unsplit small-M tile
+    assert ws(30720, 2048, 5888) == 0                    # C3: the large-tile kernels
+    assert ws(160, 8192, 2048, L.EPI_STORE) == 0         # plain store: never the small-M plan
+    assert lib.echo_set_policy_rows(8, 1) == 0
+    try:
+        assert ws(160, 2048, 5888) == 0                  # planned as 1280 rows: unsplit
+    finally:
+        assert lib.echo_set_policy_rows(1, 1) == 0
+    assert ws(160, 2048, 5888) == 4 * 160 * 2048 * 4
+    assert lib.echo_set_policy_rows(1, 2) != 0
+    assert lib.echo_attention_set_combine(4) != 0 and lib.echo_attention_set_combine(-1) != 0
+    assert lib.echo_attention_set_combine(0) == 0 and lib.echo_attention_set_combine(2) == 0
