@@ -2709,6 +2709,11 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
     if (a->epilogue != ECHO_EPI_RESID || a->batch != 1 || !a->mod_shift || !a->mod_scale1 || a->ldc != a->N ||
         a->ld_mod != a->N)
       return ECHO_EINVAL;
+    {  // the normalised rows may not overlap the residual rows they are computed from
+      const uintptr_t es = a->dtype == ECHO_F32 ? 4 : 2, bytes = (uintptr_t)a->M * a->N * es;
+      const uintptr_t c0 = (uintptr_t)a->C, m0 = (uintptr_t)a->mod_out;
+      if (m0 < c0 + bytes && c0 < m0 + bytes) return ECHO_EINVAL;
+    }
     const bool aligned = (((uintptr_t)a->mod_out | (uintptr_t)a->mod_shift | (uintptr_t)a->mod_scale1) & 15) == 0;
     int c = 0, S = 1;
     if (sk_tile(a->tile)) {

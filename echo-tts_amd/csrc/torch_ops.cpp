@@ -225,6 +225,11 @@ void gemm_launch(const Tensor& a, const Tensor& w, const Tensor& out, const opti
     TORCH_CHECK(epilogue == ECHO_EPI_RESID && s.batch == 1 && out.is_contiguous() && mod->xn.is_contiguous() &&
                     mod->xn.sizes() == out.sizes() && mod->xn.scalar_type() == a.scalar_type(),
                 "echo_hip.gemm_resid_norm: one batch, contiguous h / xn of equal shape and the model dtype");
+    {
+      const uintptr_t nb = (uintptr_t)out.numel() * out.element_size();
+      const uintptr_t h0 = (uintptr_t)out.data_ptr(), x0 = (uintptr_t)mod->xn.data_ptr();
+      TORCH_CHECK(x0 >= h0 + nb || h0 >= x0 + nb, "echo_hip.gemm_resid_norm: xn overlaps h");
+    }
     for (const Tensor* v : {&mod->shift, &mod->scale1})
       TORCH_CHECK(v->dim() == 1 && v->numel() == s.N && v->is_contiguous() && v->scalar_type() == a.scalar_type(),
                   "echo_hip.gemm_resid_norm: shift / scale1 must be contiguous [N] of the model dtype");

@@ -1012,6 +1012,9 @@ def test_gemm_resid_norm_bitwise(M, K):
     assert torch.equal(fx, ops.adaln_modulate(hr, sh[:1024].contiguous(), s1[:1024].contiguous(), eps))
     with pytest.raises(RuntimeError):  # shift must be [N]
         ops.gemm_resid_norm(a, w, h0.clone(), g, sh[:1024], s1, eps, torch.empty_like(h0))
+    with pytest.raises(RuntimeError):  # xn may not overlap h
+        hh = h0.clone()
+        ops.gemm_resid_norm(a, w, hh, g, sh, s1, eps, hh)
     # fp32 (parity mode): GEMM + the generic modulate kernel
     af, wf, hf, gf, shf, s1f = (t.float() for t in (a, w[:512], h0[:, :512], g[:512], sh[:512], s1[:512]))
     hr = hf.clone()
