@@ -1324,28 +1324,61 @@ __device__ void attn_combine_unit(const Args& a, const float* __restrict__ ws, i
   const int row = rh / a.heads, head = rh % a.heads;
   const int64_t per_split = (int64_t)a.rows * a.heads * 128 * a.n_q;
   const float* ml = ws + nsp * per_split;
+  // the gate and, for up to 4 splits (every policy split count), every split's (m, l) and partial O are loaded
+  // before any of them is used: one memory round trip instead of one per split; the arithmetic below runs in
+  // the same order either way
+  uint4 g4 = make_uint4(0, 0, 0, 0);
+  if (a.gate)
+    g4 = *(const uint4*)((const bf16_t*)a.gate + ECHO_QROW(a, row) * a.g_ld_batch + (int64_t)qi * a.g_ld_tok +
+                         head * 128 + 8 * c8);
+  constexpr int NB = 4;
+  float2 mlb[NB];
+  float4 lob[NB], hib[NB];
+  if (nsp <= NB) {
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+      if (s < nsp) {
+        const int64_t it = (int64_t)s * a.rows * a.heads + rh;
+        const float* wo = ws + it * 128 * a.n_q;
+        mlb[s] = *(const float2*)(ml + (it * a.n_q + qi) * 2);
+        lob[s] = *(const float4*)(wo + ((int64_t)(2 * c8) * a.n_q + qi) * 4);
+        hib[s] = *(const float4*)(wo + ((int64_t)(2 * c8 + 1) * a.n_q + qi) * 4);
+      }
+    }
+  }
   float mx = -INFINITY;
-  for (int s = 0; s < nsp; ++s) mx = fmaxf(mx, ml[(((int64_t)s * a.rows * a.heads + rh) * a.n_q + qi) * 2]);
+  if (nsp <= NB) {
+#pragma unroll
+    for (int s = 0; s < NB; ++s)
+      if (s < nsp) mx = fmaxf(mx, mlb[s].x);
+  } else {
+    for (int s = 0; s < nsp; ++s) mx = fmaxf(mx, ml[(((int64_t)s * a.rows * a.heads + rh) * a.n_q + qi) * 2]);
+  }
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, l = 0.f;
-  for (int s = 0; s < nsp; ++s) {
-    const int64_t it = (int64_t)s * a.rows * a.heads + rh;
-    const float2 m_l = *(const float2*)(ml + (it * a.n_q + qi) * 2);
-    if (m_l.x == -INFINITY) continue;  // split without a visible key for this query
+  auto add = [&](float2 m_l, float4 lo, float4 hi) __attribute__((always_inline)) {
+    if (m_l.x == -INFINITY) return;  // split without a visible key for this query
     const float wgt = __builtin_amdgcn_exp2f(m_l.x - mx);
-    const float* wo = ws + it * 128 * a.n_q;
-    const float4 lo = *(const float4*)(wo + ((int64_t)(2 * c8) * a.n_q + qi) * 4);
-    const float4 hi = *(const float4*)(wo + ((int64_t)(2 * c8 + 1) * a.n_q + qi) * 4);
     acc[0] += wgt * lo.x; acc[1] += wgt * lo.y; acc[2] += wgt * lo.z; acc[3] += wgt * lo.w;
     acc[4] += wgt * hi.x; acc[5] += wgt * hi.y; acc[6] += wgt * hi.z; acc[7] += wgt * hi.w;
     l += wgt * m_l.y;
+  };
+  if (nsp <= NB) {
+#pragma unroll
+    for (int s = 0; s < NB; ++s)
+      if (s < nsp) add(mlb[s], lob[s], hib[s]);
+  } else {
+    for (int s = 0; s < nsp; ++s) {
+      const int64_t it = (int64_t)s * a.rows * a.heads + rh;
+      const float* wo = ws + it * 128 * a.n_q;
+      add(*(const float2*)(ml + (it * a.n_q + qi) * 2), *(const float4*)(wo + ((int64_t)(2 * c8) * a.n_q + qi) * 4),
+          *(const float4*)(wo + ((int64_t)(2 * c8 + 1) * a.n_q + qi) * 4));
+    }
   }
   const float inv = 1.0f / l;
   float v[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = rbf(acc[e] * inv);
   if (a.gate) {
-    const uint4 g4 = *(const uint4*)((const bf16_t*)a.gate + ECHO_QROW(a, row) * a.g_ld_batch + (int64_t)qi * a.g_ld_tok + head * 128 +
-                                     8 * c8);
     const uint32_t gg[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
