@@ -1540,7 +1540,7 @@ struct T320Args {
   Epi ep;
 };
 
-template <int EK, int SP = 1, int PER = 0>
+template <int EK, int SP = 1, int PER = 0, int CP = 0>  // CP: cache policy of the epilogue stores (16 = sc1; A/B)
 __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
   static_assert(EK == EK_RESID || EK == EK_SWIGLU || EK == EK_HEADNORM, "320-row tiles: residual / SwiGLU / head norm");
   static_assert(!(PER && SP), "persistent form: 2 / 7 DMA split only");
@@ -1870,7 +1870,7 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
         const uint32_t off = (uint32_t)((m * ldc + nb) * 2);
 #pragma unroll
         for (int p = 0; p < FN / 2; ++p)
-          __builtin_amdgcn_raw_buffer_store_b128(swap_pair(hp[2 * p], hp[2 * p + 1]), crs, off + p * 64, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(swap_pair(hp[2 * p], hp[2 * p + 1]), crs, off + p * 64, 0, CP);
         // PER: one row fragment at a time (hipcc otherwise hoists the next fragments' table loads and spills)
         if constexpr (PER) __builtin_amdgcn_sched_barrier(0);
       }
@@ -1894,7 +1894,7 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
             q[jj] = make_uint2(pack2bf(u[0], u[1]), pack2bf(u[2], u[3]));
           }
           __builtin_amdgcn_raw_buffer_store_b128(swap_pair(q[0], q[1]), crs,
-                                                 (uint32_t)(((mb + ii * 16) * ldc + nbo + p * 32) * 2), 0, 0);
+                                                 (uint32_t)(((mb + ii * 16) * ldc + nbo + p * 32) * 2), 0, CP);
         }
       }
     } else {
@@ -1932,7 +1932,7 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
             v1 = bf2f(xr[ii & 1][p][w] >> 16) + v1;
             o[w] = pack2bf(v0, v1);
           }
-          __builtin_amdgcn_raw_buffer_store_b128(o, crs, off + p * 64, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(o, crs, off + p * 64, 0, CP);
         }
       }
     }
@@ -2373,7 +2373,7 @@ bool t320_ok(const EchoGemmArgs* a) {
 int g_gemm_t320_np = 0;  // echo_gemm_set_diag key 10: 1 = the non-persistent 320-row kernel (A/B)
 
 // PER = 1: one persistent workgroup per CU (grid = min(tiles, CUs rounded down to a multiple of 8))
-template <int SP, int PER>
+template <int SP, int PER, int CP = 0>
 int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   const int tm = a->M / 320, tn = a->N / 256;
   int grid = tm * tn;
@@ -2383,11 +2383,11 @@ int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   }
   const T320Args ta{(const bf16_t*)a->A, a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep};
   if (ek_of(a) == EK_SWIGLU)
-    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_SWIGLU, SP, PER>), dim3(grid), dim3(512), 0, s, ta);
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_SWIGLU, SP, PER, CP>), dim3(grid), dim3(512), 0, s, ta);
   else if (ek_of(a) == EK_HEADNORM)
-    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_HEADNORM, SP, PER>), dim3(grid), dim3(512), 0, s, ta);
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_HEADNORM, SP, PER, CP>), dim3(grid), dim3(512), 0, s, ta);
   else
-    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_RESID, SP, PER>), dim3(grid), dim3(512), 0, s, ta);
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_RESID, SP, PER, CP>), dim3(grid), dim3(512), 0, s, ta);
   ECHO_LAUNCH_CHECK();
   return 0;
 }
@@ -2398,11 +2398,12 @@ int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 // W2: no measurable gain). The head-norm epilogue's persistent form (spill-free since round 4: norm weights
 // and RoPE rows read at the use) from 8 tiles per CU: QKVG M = 30720 (12 per CU) 764.6 -> 753.0 us, M = 10240
 // (4 per CU) 258.5 vs 258.7 (profiles/r4_t320_headnorm_persistent.txt).
+template <int CP = 0>
 int launch_t320(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   const int64_t tiles = (int64_t)(a->M / 320) * (a->N / 256), cus = cu_count_cached();
   const int ek = ek_of(a);
   const bool per = !g_gemm_t320_np && ((ek == EK_SWIGLU && tiles >= 4 * cus) || (ek == EK_HEADNORM && tiles >= 8 * cus));
-  return per ? launch_t320_sp<0, 1>(a, ep, s) : launch_t320_sp<0, 0>(a, ep, s);
+  return per ? launch_t320_sp<0, 1, CP>(a, ep, s) : launch_t320_sp<0, 0, CP>(a, ep, s);
 }
 
 // auto pick between 320x256 and 256x256 tiles by whole rounds of the CUs: a 320-row tile does 1.25x the work
@@ -2766,8 +2767,8 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
   if (a->tile == 0 && t == 1) t = (a->dtype == ECHO_BF16 && ps_ok(a, ek_of(a)) && !g_gemm_no_ps) ? 16 : 13;
   // fused on the persistent kernel (t 16/17/18, N % 256 == 0, via ps_ok) or the 2-phase one (t 13)
   const bool hn_fused = a->dtype == ECHO_BF16 && ((t == 13 && a->N % 128 == 0) ||
-                                                   ((t == 16 || t == 17 || t == 18) && ps_ok(a, EK_HEADNORM)) ||
-                                                   ((t >= 20 && t <= 23) && t320_ok(a)));
+                                                   ((t == 16 || t == 17 || t == 18 || t == 25) && ps_ok(a, EK_HEADNORM)) ||
+                                                   ((t >= 20 && t <= 24) && t320_ok(a)));
   if (headnorm && !hn_fused) {
     // not fused for this shape / dtype: plain store, then the standalone kernel (same results)
     EchoGemmArgs b = *a;
@@ -2802,6 +2803,8 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
   if (a->tile == 21) return t320_ok(a) ? launch_t320_sp<1, 0>(a, ep, s) : ECHO_EINVAL;  // 4 / 5 DMA split (A/B)
   if (a->tile == 22) return t320_ok(a) ? launch_t320_sp<0, 0>(a, ep, s) : ECHO_EINVAL;  // one tile per workgroup
   if (a->tile == 23) return t320_ok(a) ? launch_t320_sp<0, 1>(a, ep, s) : ECHO_EINVAL;  // persistent
+  if (a->tile == 24) return t320_ok(a) ? launch_t320<16>(a, ep, s) : ECHO_EINVAL;  // sc1 (L2-bypassing) stores, A/B
+  if (a->tile == 25) return (a->dtype == ECHO_BF16 && ps_ok(a, ek_of(a))) ? launch_ps<16>(a, ep, s) : ECHO_EINVAL;
   if (a->tile == 0 && g_gemm_t320 == 0 && !g_gemm_no_colsplit && a->batch == 1 && !headnorm && t320_ok(a)) {
     const int c1 = t320_col_split(a, cu_count_cached());
     if (c1 > 0) {
