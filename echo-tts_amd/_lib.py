@@ -71,7 +71,6 @@ SIGNATURES = {
     "echo_gemm_set_diag": (i32, [i32, i32]),
     "echo_gemm_ws_bytes": (i64, [C.POINTER(GemmArgs)]),
     "echo_gemm_ws": (i32, [C.POINTER(GemmArgs), vp, i64, vp]),
-    "echo_attention_set_combine": (i32, [i32]),
     "echo_set_policy_rows": (i32, [i32, i32]),
     "echo_attention": (i32, [C.POINTER(AttnArgs), vp]),
     "echo_attention_variant": (i32, [C.POINTER(AttnArgs), i32, i32, vp, vp]),
@@ -108,7 +107,7 @@ SIGNATURES = {
     "echo_abi_struct_size": (i64, [i32]),
 }
 
-ABI_VERSION = 5  # include/echo_hip.h ECHO_ABI_VERSION
+ABI_VERSION = 6  # include/echo_hip.h ECHO_ABI_VERSION
 # ctypes mirrors of the argument structs, by echo_abi_struct_size id
 ABI_STRUCTS = {0: "GemmArgs", 1: "AttnArgs", 2: "KVSegment", 3: "StepArgs", 4: "RvqWeights"}
 

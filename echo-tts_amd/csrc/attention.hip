@@ -19,7 +19,6 @@
 // conflict-free for both the K row reads and the V transposed reads.
 #include "common.h"
 
-#include <mutex>
 #include <type_traits>
 
 // q / gate row of output row `row` (EchoAttnArgs.q_batch_mod: row groups that share one q copy)
@@ -273,7 +272,7 @@ struct SegInfo {
 // stores. Same tile math; only the summation order over keys differs from SP = 0 (fp32-close).
 template <int ABL, int NW, int ST, int KTT = 64, int PS = 0, int SP = 0>
 __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
-    attn_bf16_kernel(EchoAttnArgs a_arg, float* ws, int nsp, int* cnt) {
+    attn_bf16_kernel(EchoAttnArgs a_arg, float* ws, int nsp) {
   static_assert(!PS || (ABL == 0 && ST == 2), "persistent form: production schedule only");
   static_assert(!SP || (ABL == 0 && ST == 2 && !PS), "split-KV form: production schedule only");
   constexpr int QB = 32 * NW;
@@ -294,7 +293,6 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
   const int nitems = PS ? nqb * kargs->rows * kargs->heads : (int)blockIdx.x + 1;
   (void)ws;
   (void)nsp;
-  (void)cnt;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h2 = lane >> 5, ql = lane & 31;
@@ -646,31 +644,6 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
         }
       }
       (void)inv;
-      if (cnt) {
-        // fused combine: the last of the item's nsp split workgroups to finish merges them. Each workgroup's
-        // partial stores are released at agent scope before it counts itself in on the item's counter; the
-        // last arriver resets the counter for the next launch and acquires before reading the partials
-        // (the counters start at 0: echo_attention_split allocates and clears them once, outside capture)
-        __shared__ int s_last;
-        __threadfence();
-        __syncthreads();
-        if (tid == 0) {
-          int* c = cnt + (row * a.heads + head) * nqb + qb;
-          const int last = __hip_atomic_fetch_add(c, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nsp - 1;
-          if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          s_last = last;
-        }
-        __syncthreads();
-        if (s_last) {
-          __threadfence();
-          const int rh = row * a.heads + head;
-          // query fastest, as attn_combine_kernel: the partial reads are contiguous over the queries
-          for (int u = tid; u < QB * 16; u += 64 * NW) {
-            const int qq = q0 + u % QB, c8 = u / QB;
-            if (qq < a.n_q) attn_combine_unit(a, ws, nsp, rh, qq, c8);
-          }
-        }
-      }
     } else if constexpr (PS) {
       // (the persistent form keeps the per-lane epilogue: the row form's LDS transposition needs a
       // barrier before the next item's DMA and spills around the item loop — 179 vs 154 us, R = 16)
@@ -748,32 +721,17 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
 #pragma clang diagnostic ignored "-Winline-asm"
 #include "attn_pl.inc"
 
-// ABL (timing ablations, variants 12-19; results wrong except 32): 1 no loop DMA, 2 no X body, 4 no Y body,
-// 8 no end-of-tile wait + barrier, 16 no tile loop; 32 (diagnostic, results right): CFG rows of one prompt
-// (r, r + B, r + 2B; B = segment 1's batch_mod) adjacent in the block order; 64 (diagnostic, results right):
-// longest-first block order per XCD; 128 (results right): V(t+1)'s DMA between the X and Y bodies (NK = NV = 2)
+// ABL (timing ablations, variants 12-16; results wrong): 1 no loop DMA, 2 no X body, 4 no Y body,
+// 8 no end-of-tile wait + barrier, 16 no tile loop.
 // NW: waves per workgroup (4: 128 queries, two workgroups per CU; 8: 256 queries, one workgroup per CU, each
-// K/V tile staged once for twice the queries)
-// NK / NV: K / V tiles in the LDS ring (16 KiB each). K(j) lives in slot j % NK, V(j) in slot j % NV. At the
-// top of tile t the slots of K(t) and V(t - 1) are free (read before the previous barrier) and take K(t + NK)
-// and V(t + NV - 1); the end-of-tile wait needs only K(t + 2) and V(t + 1) (read in tile t + 1), so with
-// NK, NV >= 3 the DMA issued in tile t stays in flight across the barrier (a counted vmcnt: V is issued first,
-// K second, both younger than every piece the wait needs) and each tile's loads get two tiles of latency
-// budget instead of one (NK = NV = 2 waits vmcnt(0) for the loads it issued at its own top). LDS: (NK + NV) x
-// 16 KiB — 2 + 2 and 3 + 2 keep two workgroups per CU, 3 + 3 and 4 + 4 one.
-// SP = 1: the split-KV form (attn_bf16_kernel's SP = 1 layout: split s of nsp walks tiles [s n / nsp, (s+1) n / nsp)
-// of the item's flat tile list and stores its unnormalised partial to `ws` for attn_combine_kernel): bitwise the
-// compiler-scheduled split kernel's partials, with this kernel's pipelined tile loop.
-template <int ABL, int NW = 4, int NK = 2, int NV = 2, int SP = 0>
-__global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __attribute__((amdgpu_num_vgpr(96)))
-    attn_pl_kernel(EchoAttnArgs a_arg, float* ws, int nsp) {
-  static_assert(!SP || (ABL == 0 && NW == 4 && NK == 2 && NV == 2), "split-KV form: production schedule only");
-  constexpr int QB = 32 * NW, DPT = 16 / NW, KTT = KT;
-  static_assert(NK >= 2 && NV >= 2 && NK <= 4 && NV <= 4, "ring slots (attn_pl.inc MAX_SLOTS)");
-  static_assert(!(ABL & 128) || (NK == 2 && NV == 2), "ablation 128 is defined on the 2 + 2 ring");
-  // unroll period lcm(2, NK, NV): slots and score buffers are literals of the bodies (3 with 4 would need 12)
-  constexpr int PER = (NK == 3 || NV == 3) ? 6 : (NK == 4 || NV == 4) ? 4 : 2;
-  static_assert(PER % NK == 0 && PER % NV == 0, "unsupported ring combination");
+// K/V tile staged once for twice the queries — variant 20, slower: DESIGN.md §3).
+// Measured and removed (round 5 prune; numbers in DESIGN.md §3 / §7): K / V rings of 3 + 2, 3 + 3, 4 + 4 and
+// 2 + 3 slots with counted waits across the barrier; V(t+1)'s DMA between the X and Y bodies; CFG-adjacent
+// and longest-first block orders; the split-KV form of this kernel (2-4 % slower than attn_bf16_kernel's).
+template <int ABL, int NW = 4>
+__global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgpu_num_vgpr(96)))
+    attn_pl_kernel(EchoAttnArgs a_arg) {
+  constexpr int QB = 32 * NW, DPT = 16 / NW, KTT = KT, NK = 2, NV = 2;
   __shared__ __attribute__((aligned(16))) bf16_t lds[(NK + NV) * KT * 128];  // K slots | V slots
 
   using KArgs = const __attribute__((address_space(4))) EchoAttnArgs;
@@ -782,26 +740,8 @@ __global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __a
   const int nqb = (a.n_q + QB - 1) / QB;
   const int L = remap_xcd(blockIdx.x, gridDim.x);
   const int qb = L % nqb;
-  const int Lr = SP ? L / (nqb * nsp) : L / nqb;  // rows fastest (see attn_bf16_kernel)
-  const int sp = SP ? (L / nqb) % nsp : 0;
-  (void)ws;
-  int row = Lr % a.rows;
-  if constexpr ((ABL & 32) != 0) {
-    const int B = a.nseg > 1 ? a.seg[1].batch_mod : a.rows;
-    if (a.rows == 3 * B) row = (row % 3) * B + row / 3;
-  }
-  int head = Lr / a.rows;
-  if constexpr ((ABL & 64) != 0) {
-    // diagnostic order (results right): each XCD's chunk holds heads/8 whole heads, rows slowest, the three
-    // CFG row groups in the order cond, uncond-speaker, uncond-text (longest first at C3's lengths)
-    if (a.heads % 8 == 0) {
-      const int chunk = gridDim.x >> 3, x = L / chunk, p = L - x * chunk, hpx = a.heads >> 3;
-      const int rest = p / nqb, slot = rest / hpx;
-      head = x * hpx + rest % hpx;
-      const int B = a.nseg > 1 ? a.seg[1].batch_mod : a.rows;
-      row = (a.rows == 3 * B) ? (slot < B ? slot : slot < 2 * B ? slot + B : slot - B) : slot;
-    }
-  }
+  const int Lr = L / nqb;  // rows fastest (see attn_bf16_kernel)
+  const int row = Lr % a.rows, head = Lr / a.rows;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h2 = lane >> 5, ql = lane & 31;
@@ -818,12 +758,6 @@ __global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __a
   Cursor kc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // K DMA (NK - 1 tiles ahead of the QK)
   Cursor vc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // V DMA (NV - 1 tiles ahead of the PV)
   Cursor mc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // the tile whose scores are masked / maxed
-  if constexpr (SP) {
-    // this split's tile range of the flat list (scalar cursor walk; <= ~20 tiles)
-    const int tb = sp * ntiles / nsp, te = (sp + 1) * ntiles / nsp;
-    for (int i = 0; i < tb; ++i) { advance(kc); advance(vc); advance(mc); }
-    ntiles = te - tb;
-  }
 
   const int dr = lane >> 4, dp = lane & 15;
   // one tile's share of this wave (DPT pieces) into slot `slot` of the K (part 0) or V (part 1) ring
@@ -888,28 +822,13 @@ __global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __a
   };
 
   pl_zero_o();
-  // prologue: K(0), V(0), K(1) — needed before tile 0's loop iteration — then V(1 .. NV-2), K(2 .. NK-1), which
-  // may stay in flight; scores, mask and max of tile 0
+  // prologue: K(0), V(0), K(1) — needed before tile 0's loop iteration; scores, mask and max of tile 0
   if (ntiles > 0) { dma_part(kc, 0, 0); dma_part(vc, 1, 0); }
   if (ntiles > 1) dma_part(kc, 0, 1);
-#pragma unroll
-  for (int j = 1; j <= NV - 2; ++j)
-    if (j < ntiles) dma_part(vc, 1, j);
-#pragma unroll
-  for (int j = 2; j <= NK - 1; ++j)
-    if (j < ntiles) dma_part(kc, 0, j);
   // Q and the prologue DMA in flight together: one wait (hipcc's vmcnt(0) for Q covers the DMA issued after it)
 #pragma unroll
   for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));
-  {
-    const int younger = (min(NV - 1, ntiles) - 1 > 0 ? min(NV - 1, ntiles) - 1 : 0) +
-                        (min(NK, ntiles) - 2 > 0 ? min(NK, ntiles) - 2 : 0);  // pieces issued after K(1)
-    if (NK + NV == 4 || younger == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(DPT) : "memory");
-    else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * DPT) : "memory");
-    else if (younger == 3) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(3 * DPT) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(4 * DPT) : "memory");
-  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   if (ntiles > 0) {
     if (wact) {
       pl_qk_cs<0, 0>(qf, ka);
@@ -924,34 +843,20 @@ __global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __a
   asm volatile("s_barrier" ::: "memory");  // every wave's K(0) reads are done: slot 0 takes K(NK)
 
   auto iter = [&](int t, auto unr) __attribute__((always_inline)) {
-    constexpr int U = decltype(unr)::value;  // t mod PER
-    constexpr int P = U & 1;                 // score buffer of tile t
-    constexpr int KS = (U + 1) % NK;         // K slot of tile t + 1 (its QK runs in X(t))
-    constexpr int VS = U % NV;               // V slot of tile t (its PV runs in Y(t))
-    int issued = 0;                          // DMA tiles of this wave issued at this tile's top
-    if constexpr (NK == 2 && NV == 2) {
-      if (t + 2 < ntiles && !(ABL & 1)) dma_part(kc, 0, P);      // K(t+2) -> K slot t & 1 (K(t) was read in X(t-1))
-      // V(t+1) -> V slot (t+1) & 1 (V(t-1) was read in Y(t-1)); ABL 128: issued between X(t) and Y(t) instead
-      if (!(ABL & 128) && t + 1 < ntiles && !(ABL & 1)) dma_part(vc, 1, 1 - P);
-    } else if constexpr (NK == 2) {
-      // K(t+2) first (waited at this tile's end), then V(t+NV-1), which stays in flight across the barrier
-      if (t + NK < ntiles && !(ABL & 1)) dma_part(kc, 0, U % NK);
-      if (t + NV - 1 < ntiles && !(ABL & 1)) { dma_part(vc, 1, (U + NV - 1) % NV); ++issued; }
-    } else {
-      if (t + NV - 1 < ntiles && !(ABL & 1)) { dma_part(vc, 1, (U + NV - 1) % NV); ++issued; }  // V first
-      if (t + NK < ntiles && !(ABL & 1)) { dma_part(kc, 0, U % NK); ++issued; }
-    }
+    constexpr int P = decltype(unr)::value;  // t & 1: the score buffer of tile t
+    constexpr int KS = 1 - P;                // K slot of tile t + 1 (its QK runs in X(t))
+    constexpr int VS = P;                    // V slot of tile t (its PV runs in Y(t))
+    if (t + 2 < ntiles && !(ABL & 1)) dma_part(kc, 0, P);      // K(t+2) -> K slot t & 1 (K(t) was read in X(t-1))
+    if (t + 1 < ntiles && !(ABL & 1)) dma_part(vc, 1, 1 - P);  // V(t+1) -> V slot (t+1) & 1 (V(t-1) read in Y(t-1))
     const float msc = m_run == -INFINITY ? 0.f : -m_run * sl2;
     float ps;
     if (!wact) {
       if (t + 1 < ntiles) advance(mc);
-      if ((ABL & 128) && !(ABL & 1) && t + 1 < ntiles) dma_part(vc, 1, 1 - P);
     } else if (t + 1 < ntiles) {
       ps = 0.f;
       if constexpr (!(ABL & 2)) pl_x_cs<P, KS>(qf, ka, sl2, msc, ps);
       l_run += ps;
       mask_tile(std::integral_constant<int, 1 - P>{});
-      if ((ABL & 128) && !(ABL & 1)) dma_part(vc, 1, 1 - P);
       float mx = 0.f, ma;
       if constexpr (!(ABL & 4)) pl_y_cs<P, VS>(va, mx, ma);
       decide(mx);
@@ -960,67 +865,20 @@ __global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __a
       l_run += ps;
       pl_yl_cs<P, VS>(va);
     }
-    if constexpr (!(ABL & 8)) {
-      // K(t+2) and V(t+1) must have landed (every wave's share, then the barrier); with NK, NV >= 3 the tiles
-      // issued at this tile's top are younger than both and stay in flight (NV == 2: V(t+1) is this tile's V
-      // issue, so only the K issued after it may stay; NK == 2, NV >= 3: K(t+2) is issued first, V(t+NV-1)
-      // after it stays in flight)
-      const int keep = (NK == 2 && NV == 2) ? 0 : NK == 2 ? issued : NV == 2 ? (issued == 2 ? 1 : 0) : issued;
-      if (keep == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      else if (keep == 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(DPT) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * DPT) : "memory");
-    }
+    // K(t+2) and V(t+1) must have landed (every wave's share, then the barrier)
+    if constexpr (!(ABL & 8)) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   };
   if (ABL & 16) ntiles = 0;
-  for (int t = 0; t < ntiles; t += PER) {
+  for (int t = 0; t < ntiles; t += 2) {
     iter(t, std::integral_constant<int, 0>{});
     if (t + 1 >= ntiles) break;
     iter(t + 1, std::integral_constant<int, 1>{});
-    if constexpr (PER >= 4) {
-      if (t + 2 >= ntiles) break;
-      iter(t + 2, std::integral_constant<int, 2 % PER>{});
-      if (t + 3 >= ntiles) break;
-      iter(t + 3, std::integral_constant<int, 3 % PER>{});
-    }
-    if constexpr (PER == 6) {
-      if (t + 4 >= ntiles) break;
-      iter(t + 4, std::integral_constant<int, 4 % PER>{});
-      if (t + 5 >= ntiles) break;
-      iter(t + 5, std::integral_constant<int, 5 % PER>{});
-    }
   }
 
   // ---- epilogue (attn_bf16_kernel's row layout): normalise, round, transpose through LDS, gate, store
   const float lt = halves_sum(l_run);
   const float inv = 1.0f / lt;
   const int nv = a.n_q - (q0 + w * 32);  // wave-uniform
-  if constexpr (SP) {
-    // unnormalised partial, attn_bf16_kernel's SP layout: chunk c = d / 4 of query qi at ws[it][c][qi], then
-    // (m in exp2 units, l) per query after all splits' O
-    const int qi = q0 + w * 32 + ql;
-    if (qi < a.n_q) {
-      const int64_t it = ((int64_t)sp * a.rows + row) * a.heads + head;
-      float* wo = ws + it * 128 * a.n_q;
-      float od[16];
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        if (dt == 0) pl_get_o_0(od); else if (dt == 1) pl_get_o_1(od); else if (dt == 2) pl_get_o_2(od); else pl_get_o_3(od);
-#pragma unroll
-        for (int rg = 0; rg < 4; ++rg) {
-          const int c = dt * 8 + 2 * rg + h2;
-          *(float4*)(wo + ((int64_t)c * a.n_q + qi) * 4) =
-              make_float4(od[4 * rg], od[4 * rg + 1], od[4 * rg + 2], od[4 * rg + 3]);
-        }
-      }
-      if (h2 == 0) {
-        float* wml = ws + (int64_t)nsp * a.rows * a.heads * 128 * a.n_q + (it * a.n_q + qi) * 2;
-        *(float2*)wml = make_float2(m_run == -INFINITY ? -INFINITY : m_run * sl2, lt);
-      }
-    }
-    (void)inv;
-    (void)nv;
-    return;
-  }
   if (nv > 0) {
     uint4 v4[8];
     auto pack_dt = [&](const float (&od)[16], int dt) __attribute__((always_inline)) {
@@ -1069,256 +927,7 @@ __global__ void __launch_bounds__(64 * NW, (NW == 8 || NK + NV > 5) ? 1 : 2) __a
 }
 #pragma clang diagnostic pop
 
-// ----------------------------------------------------------------------------- software-pipelined
-// Same tile math, LDS image and numerics as attn_bf16_kernel<0,4,2>, scheduled so that every wave
-// overlaps its own MFMA and VALU work (cdna_hip_programming.md T15), two workgroups per CU:
-//   phase A of iteration t: S(t+1) = K(t+1).Q^T (16 MFMA)  ||  softmax finish of tile t
-//                           (exp2, row sums, bf16 pack of P(t))
-//   phase B of iteration t: O^T += V(t)^T.P(t) (16 MFMA)   ||  row max of S(t+1)
-// K and V have separate double buffers: K(t+2) and V(t+1) are issued at the top of iteration t
-// (their slots held K(t) and V(t-1), both consumed in iteration t-1); one barrier per iteration.
-// sched_group_barrier pins the MFMA / LDS-read / VALU interleave (T19), reads 2-4 MFMAs ahead.
-constexpr int SG_MFMA = 0x8, SG_VALU = 0x2, SG_DSR = 0x100, SG_TRANS = 0x400;
-
-template <int ABL>
-__global__ void __launch_bounds__(256, 2) attn_pipe_kernel(EchoAttnArgs a) {
-  constexpr int NW = 4, QB = 128, DPT = 4, KTT = KT;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[4 * KT * 128];  // K slot 0, 1 | V slot 0, 1
-
-  const int nqb = (a.n_q + QB - 1) / QB;
-  const int L = remap_xcd(blockIdx.x, gridDim.x);
-  const int qb = L % nqb;
-  const int row = (L / nqb) % a.rows;  // rows fastest (see attn_bf16_kernel)
-  const int head = L / (nqb * a.rows);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h2 = lane >> 5, ql = lane & 31;
-  const int q0 = qb * QB;
-  const int qi = q0 + w * 32 + ql;
-  const int qc = min(qi, a.n_q - 1);
-
-  const bf16_t* qp = (const bf16_t*)a.q + ECHO_QROW(a, row) * a.q_ld_batch + (int64_t)qc * a.q_ld_tok + head * 128;
-  bf16x8 qf[8];
-#pragma unroll
-  for (int ds = 0; ds < 8; ++ds) qf[ds] = *(const bf16x8*)(qp + 16 * ds + 8 * h2);
-#pragma unroll
-  for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));
-
-  ECHO_SEG_TABLE()
-  ECHO_CURSOR_ADVANCE()
-  Cursor kc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // K DMA (two tiles ahead of compute)
-  Cursor vc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // V DMA (one tile ahead)
-  Cursor mc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // masking of the tile whose scores are formed
-
-  // K (part 0) or V (part 1) of the cursor's next tile into `slot` (16 wave-instructions of 1 KiB)
-  const int dr = lane >> 4, dp = lane & 15;
-  auto dma_part = [&](Cursor& c, int part, int slot) __attribute__((always_inline)) {
-    advance(c);
-    const int last = c.kend - 1 - c.t0;
-    const bf16_t* base = (part ? c.vb : c.kb) + (int64_t)c.t0 * c.ld;
-#pragma unroll
-    for (int i = 0; i < DPT; ++i) {
-      const int r = (i * NW + w) * 4 + dr;
-      const uint32_t voff = (uint32_t)(min(r, last) * c.ld + ((dp ^ swz(r)) * 8)) * 2u;
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(
-          lds_addr_of(lds + (part * 2 + slot) * KT * 128 + ((i * NW + w) * 4) * 128));
-      glds16s(base, voff, dst);
-    }
-  };
-  auto mask_tile = [&](f32x16 (&st)[2]) __attribute__((always_inline)) {
-    advance(mc);
-    if (mc.t0 + KT <= mc.kend && !mc.causal) return;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = mc.t0 + kk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
-        const bool ok = key < mc.kend && (!mc.causal || key <= qi);
-        st[kk][r] = ok ? st[kk][r] : -INFINITY;
-      }
-  };
-  auto qk_tile = [&](const bf16_t* Ks, f32x16 (&st)[2]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) st[kk][r] = 0.f;
-      const int kr = kk * 32 + ql;
-#pragma unroll
-      for (int ds = 0; ds < 8; ++ds) {
-        const bf16x8 kf = *(const bf16x8*)(Ks + kr * 128 + (((2 * ds + h2) ^ swz(kr)) * 8));
-        st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], st[kk], 0, 0, 0);
-      }
-    }
-  };
-  auto row_max = [&](const f32x16 (&st)[2]) __attribute__((always_inline)) -> float {
-    float m0 = -INFINITY, m1 = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      m0 = fmaxf(m0, fmaxf(st[0][r], st[0][r + 1]));
-      m1 = fmaxf(m1, fmaxf(st[1][r], st[1][r + 1]));
-    }
-    // permlane32_swap(x, x): r[0] = {x.lo, x.lo}, r[1] = {x.hi, x.hi} -> both halves in every lane
-    const float m = fmaxf(m0, m1);
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
-    return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-  };
-
-  f32x16 o[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
-  const float sl2 = a.scale * 1.4426950408889634f;
-  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-
-  // iteration t: sc = raw scores of tile t (masked), mxc = their row max; produces sn / mxn for t+1
-  auto iter = [&](int t, f32x16 (&sc)[2], float mxc, f32x16 (&sn)[2], float& mxn) __attribute__((always_inline)) {
-    const bool has_next = t + 1 < ntiles;
-    if (!(ABL & 1)) {
-      if (t + 2 < ntiles) dma_part(kc, 0, t & 1);   // K(t+2) into the slot of K(t)
-      if (has_next) dma_part(vc, 1, (t + 1) & 1);    // V(t+1) into the slot of V(t-1)
-    }
-    const bf16_t* Kn = lds + ((t + 1) & 1) * KT * 128;
-    const bf16_t* Vc = lds + (2 + (t & 1)) * KT * 128;
-    const float m_new = fmaxf(m_run, mxc);
-    const float msc = m_new == -INFINITY ? 0.f : -m_new * sl2;
-    if (__any(m_new != m_run)) {  // otherwise alpha == 1 exactly for every lane
-      const float alpha = __builtin_amdgcn_exp2f(__builtin_fmaf(m_run, sl2, msc));
-      l_run *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-    }
-    m_run = m_new;
-
-    // ---- phase A: QK(t+1) || exp / row sum / pack of P(t)
-    bf16x8 pf[4];
-    float ps0 = 0.f, ps1 = 0.f;
-    auto softmax_finish = [&]() __attribute__((always_inline)) {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kk][8 * s2 + j], sl2, msc));
-            if (j & 1) ps1 += pv; else ps0 += pv;
-            pf[kk * 2 + s2][j] = (__bf16)pv;
-          }
-    };
-    if (has_next) {
-      qk_tile(Kn, sn);
-      softmax_finish();
-      // K fragment reads 4 MFMAs ahead; per MFMA gap 2 exp + 3 other VALU (MI355X_MICROARCH
-      // 'vector-instruction ISSUE cost': 2x8 + 3x4 + the MFMA's 8 stays near the 32-cycle gap)
-      __builtin_amdgcn_sched_group_barrier(SG_DSR, 4, 0);
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
-        if (k < 12) __builtin_amdgcn_sched_group_barrier(SG_DSR, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(SG_TRANS, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(SG_VALU, 3, 0);
-      }
-    } else {
-      softmax_finish();
-    }
-    l_run += ps0 + ps1;
-
-    // ---- phase B: PV(t) || row max of S(t+1) (garbage and unused when there is no t+1)
-    if (has_next) mask_tile(sn);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const int key0 = kk * 32 + 16 * s2 + 4 * h2;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const int ch = 4 * dt + 2 * (g & 1) + (p4 >> 1);
-          const int r0 = key0 + q4, r1 = key0 + 8 + q4;
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(Vc + r0 * 128 + ((ch ^ swz(r0)) * 8) + (p4 & 1) * 4));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(Vc + r1 * 128 + ((ch ^ swz(r1)) * 8) + (p4 & 1) * 4));
-          typedef __attribute__((ext_vector_type(8))) short s16x8;
-          const s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf[kk * 2 + s2], o[dt],
-                                                           0, 0, 0);
-        }
-      }
-    mxn = row_max(sn);
-    // V^T transposed reads (2 per MFMA) 2 MFMAs ahead; the row max fills the gaps
-    __builtin_amdgcn_sched_group_barrier(SG_DSR, 4, 1);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 1);
-      if (k < 14) __builtin_amdgcn_sched_group_barrier(SG_DSR, 2, 1);
-      __builtin_amdgcn_sched_group_barrier(SG_VALU, 2, 1);
-    }
-    // K(t+2) and V(t+1) landed (this wave's share) ... and everyone's; slots of K(t+1)/V(t) free
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  };
-
-  f32x16 sa[2], sb[2];
-  float mxa = -INFINITY, mxb = -INFINITY;
-  // prologue: K0 V0 K1; QK(0) and its row max; then K slot 0 is refilled (tile 2) in iteration 0
-  if (ntiles > 0) { dma_part(kc, 0, 0); dma_part(vc, 1, 0); }
-  if (ntiles > 1) dma_part(kc, 0, 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (ntiles > 0) {
-    qk_tile(lds, sa);
-    mask_tile(sa);
-    mxa = row_max(sa);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int t = 0; t < ntiles; t += 2) {
-    iter(t, sa, mxa, sb, mxb);
-    if (t + 1 >= ntiles) break;
-    iter(t + 1, sb, mxb, sa, mxa);
-  }
-
-  // ---- epilogue: normalise, round, gate, store (4 consecutive d per register group)
-  const auto lsw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
-  const float lt = __uint_as_float(lsw[0]) + __uint_as_float(lsw[1]);
-  const float inv = 1.0f / lt;
-  if (qi >= a.n_q) return;
-  bf16_t* op = (bf16_t*)a.out + row * a.o_ld_batch + (int64_t)qi * a.o_ld_tok + head * 128;
-  const bf16_t* gp = a.gate ? (const bf16_t*)a.gate + ECHO_QROW(a, row) * a.g_ld_batch + (int64_t)qi * a.g_ld_tok + head * 128
-                            : nullptr;
-  uint2 gg[16];
-  if (gp) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) gg[k] = *(const uint2*)(gp + (k >> 2) * 32 + 8 * (k & 3) + 4 * h2);
-  }
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int rg = 0; rg < 4; ++rg) {
-      const int d = dt * 32 + 8 * rg + 4 * h2;
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = rbf(o[dt][4 * rg + e] * inv);
-      if (gp) {
-        const uint2 g2 = gg[dt * 4 + rg];
-        const float gv[4] = {bf2f(g2.x & 0xffffu), bf2f(g2.x >> 16), bf2f(g2.y & 0xffffu), bf2f(g2.y >> 16)};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = rbf(v[e] * rbf(sigmoid_f(gv[e])));
-      }
-      *(uint2*)(op + d) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
-    }
-}
-
-// ----------------------------------------------------------------------------- split-KV combine
-// One thread per (query, 8 output columns): M = max_s m_s, w_s = 2^(m_s - M),
-// out = round(round(sum_s w_s O_s / sum_s w_s l_s) * round(sigmoid(gate))) — the roundings of
-// attn_pack_out. 16 queries x 16 column groups per 256-thread block (query fastest: the partial
-// reads are 256-B runs, the 16-B output stores fill whole rows across the block).
-// one (query qi, 8 output columns c8) unit of (row, head) rh: also the fused combine of the split kernel's last
-// workgroup (attn_bf16_kernel, cnt != nullptr), so both forms give the same bits
+// one (query qi, 8 output columns c8) unit of (row, head) rh of the split-KV combine
 template <class Args>
 __device__ void attn_combine_unit(const Args& a, const float* __restrict__ ws, int nsp, int rh, int qi, int c8) {
   const int row = rh / a.heads, head = rh % a.heads;
@@ -1521,7 +1130,7 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
   const int qb = (cfg == 1 || cfg == 2 || cfg == 4) ? 256 : 128;
   const dim3 grid(attn_grid(a, qb));
 #define ECHO_ATTN_LAUNCH(A, NW, ST, ...) \
-  hipLaunchKernelGGL((attn_bf16_kernel<A, NW, ST, ##__VA_ARGS__>), grid, dim3(64 * NW), 0, s, *a, (float*)nullptr, 1, (int*)nullptr)
+  hipLaunchKernelGGL((attn_bf16_kernel<A, NW, ST, ##__VA_ARGS__>), grid, dim3(64 * NW), 0, s, *a, (float*)nullptr, 1)
 #define ECHO_ATTN_ABLS(NW, ST)                        \
   switch (abl) {                                      \
     case 0: ECHO_ATTN_LAUNCH(0, NW, ST); break;       \
@@ -1549,52 +1158,37 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 2: ECHO_ATTN_ABLS(8, 3); break;
     case 3: ECHO_ATTN_ABLS(4, 0); break;
     case 4: ECHO_ATTN_ABLS(8, 0); break;
-    case 5:
-      if (abl == 1) hipLaunchKernelGGL((attn_pipe_kernel<1>), grid, dim3(256), 0, s, *a);
-      else if (abl == 0) hipLaunchKernelGGL((attn_pipe_kernel<0>), grid, dim3(256), 0, s, *a);
-      else return ECHO_EINVAL;
-      break;
     case 8: {  // persistent form: two workgroups per CU
       if (abl) return ECHO_EINVAL;
       const int ps_grid = attn_ps_grid(grid.x);
       if (ps_grid <= 0) return ECHO_EINVAL;
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a, (float*)nullptr, 1, (int*)nullptr);
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a, (float*)nullptr, 1);
       break;
     }
     case 6: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 2, 32); break;
     case 9:  // 2 waves x 32 queries per workgroup (production for launches that cannot fill the CUs)
       if (abl) return ECHO_EINVAL;
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 2, 2>), dim3(attn_grid(a, 64)), dim3(128), 0, s, *a, (float*)nullptr, 1, (int*)nullptr);
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 2, 2>), dim3(attn_grid(a, 64)), dim3(128), 0, s, *a, (float*)nullptr, 1);
       break;
     case 7: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 3, 32); break;
     case 10: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(2048, 4, 2); break;  // per-lane epilogue
     case 11:  // asm-owned software pipeline (production for non-causal launches)
       if (abl || any_causal(a)) return ECHO_EINVAL;
-      hipLaunchKernelGGL(attn_pl_kernel<0>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1);
+      hipLaunchKernelGGL(attn_pl_kernel<0>, grid, dim3(256), 0, s, *a);
       break;
-    case 12: hipLaunchKernelGGL(attn_pl_kernel<1>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    case 13: hipLaunchKernelGGL(attn_pl_kernel<2>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    case 14: hipLaunchKernelGGL(attn_pl_kernel<4>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    case 15: hipLaunchKernelGGL(attn_pl_kernel<8>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    case 16: hipLaunchKernelGGL(attn_pl_kernel<16>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    case 17: hipLaunchKernelGGL(attn_pl_kernel<6>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    case 18: hipLaunchKernelGGL(attn_pl_kernel<7>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    case 19: hipLaunchKernelGGL(attn_pl_kernel<32>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    case 25: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<128>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    case 23: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<64>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    case 24: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL(attn_pl_kernel<32>, grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    // asm pipeline with deeper K / V rings (NK + NV slots of 16 KiB; counted waits keep each tile's DMA in
-    // flight across its barrier): 26 = 3 + 2 (80 KiB, two workgroups per CU), 27 = 3 + 3, 28 = 4 + 4 (one per CU)
-    case 26: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 3, 2>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    case 27: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 3, 3>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    case 28: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 4, 4>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
-    case 29: if (any_causal(a)) return ECHO_EINVAL; hipLaunchKernelGGL((attn_pl_kernel<0, 4, 2, 3>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1); break;
+    case 12: hipLaunchKernelGGL(attn_pl_kernel<1>, grid, dim3(256), 0, s, *a); break;
+    case 13: hipLaunchKernelGGL(attn_pl_kernel<2>, grid, dim3(256), 0, s, *a); break;
+    case 14: hipLaunchKernelGGL(attn_pl_kernel<4>, grid, dim3(256), 0, s, *a); break;
+    case 15: hipLaunchKernelGGL(attn_pl_kernel<8>, grid, dim3(256), 0, s, *a); break;
+    case 16: hipLaunchKernelGGL(attn_pl_kernel<16>, grid, dim3(256), 0, s, *a); break;
+    case 17: hipLaunchKernelGGL(attn_pl_kernel<6>, grid, dim3(256), 0, s, *a); break;
+    case 18: hipLaunchKernelGGL(attn_pl_kernel<7>, grid, dim3(256), 0, s, *a); break;
     case 20: case 21: case 22: {  // asm pipeline at 8 waves x 32 queries (21: no tile loop, 22: no X / Y bodies)
       if (any_causal(a)) return ECHO_EINVAL;
       const dim3 g8(attn_grid(a, 256));
-      if (cfg == 20) hipLaunchKernelGGL((attn_pl_kernel<0, 8>), g8, dim3(512), 0, s, *a, (float*)nullptr, 1);
-      else if (cfg == 21) hipLaunchKernelGGL((attn_pl_kernel<16, 8>), g8, dim3(512), 0, s, *a, (float*)nullptr, 1);
-      else hipLaunchKernelGGL((attn_pl_kernel<6, 8>), g8, dim3(512), 0, s, *a, (float*)nullptr, 1);
+      if (cfg == 20) hipLaunchKernelGGL((attn_pl_kernel<0, 8>), g8, dim3(512), 0, s, *a);
+      else if (cfg == 21) hipLaunchKernelGGL((attn_pl_kernel<16, 8>), g8, dim3(512), 0, s, *a);
+      else hipLaunchKernelGGL((attn_pl_kernel<6, 8>), g8, dim3(512), 0, s, *a);
       break;
     }
     default: return ECHO_EINVAL;
@@ -1622,9 +1216,9 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
     // non-causal launches (every decoder attention) run the asm-owned pipeline (attn_pl_kernel, bitwise
     // equal to attn_bf16_kernel<0, 4, 2>); causal ones (speaker / latent encoders) the compiler-scheduled kernel
     if (g_attn_pl && !any_causal(a))
-      hipLaunchKernelGGL(attn_pl_kernel<0>, dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1);
+      hipLaunchKernelGGL(attn_pl_kernel<0>, dim3(attn_grid(a, 128)), dim3(256), 0, s, *a);
     else
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1, (int*)nullptr);
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1);
   } else {
     hipLaunchKernelGGL(attn_f32_kernel, dim3(attn_grid(a, FQ)), dim3(64), 0, s, *a);
   }
@@ -1636,42 +1230,6 @@ extern int g_policy_num, g_policy_den;  // echo_set_policy_rows (gemm.hip)
 
 namespace {
 int g_attn_split_override = -1;  // echo_attention_set_split: force nsplit (diagnostics), -1 = policy
-// echo_attention_set_combine: 1 = each item's last split workgroup merges the partials. Measured slower on
-// MI355X (C2 136.2 -> 124.8, C5 at B = 1 66.8 -> 50.4 audio-s/s, profiles/r4_attn_fused_combine.txt): the
-// agent-scope release each split workgroup needs writes back its XCD's L2 (buffer_wbl2), and the merge runs
-// on one CU per item. Default 0: the separate combine kernel.
-int g_attn_fused_combine = 0;
-// echo_attention_set_combine(2 / 3): the split kernel on the compiler-scheduled (0, default) or asm-pipelined (1)
-// tile loop — bitwise the same partials; at the B = 1 policy splits the compiler-scheduled one is 2-4 % faster
-// (one workgroup per CU: 29.0 vs 29.7, 24.6 vs 25.0, 20.5 vs 21.3 us; profiles/r4_attn_split_kernels.txt)
-int g_attn_split_pl = 0;
-
-// split-KV item counters of the fused combine: one zeroed array per device, allocated on the first split launch
-// that is not being captured (a graph captured before then keeps the separate combine kernel); each item's last
-// workgroup resets its counter, so the array is all zeros between launches. Concurrent split launches on
-// different streams would share it: they must use the separate combine (echo_attention_set_combine(0)).
-constexpr int kAttnCounters = 1 << 16;
-std::mutex g_cnt_mu;
-int* g_cnt[64] = {};
-
-int* attn_counters(hipStream_t s, int64_t items) {
-  if (!g_attn_fused_combine || items > kAttnCounters) return nullptr;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> lk(g_cnt_mu);
-  if (g_cnt[dev]) return g_cnt[dev];
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
-  int* p = nullptr;
-  if (hipMalloc(&p, kAttnCounters * sizeof(int)) != hipSuccess) return nullptr;
-  if (hipMemset(p, 0, kAttnCounters * sizeof(int)) != hipSuccess) {
-    (void)hipFree(p);
-    return nullptr;
-  }
-  g_cnt[dev] = p;
-  return p;
-}
-
 int cu_count() {
   static int cus = 0;
   if (cus == 0) {
@@ -1719,13 +1277,6 @@ extern "C" int echo_attention_set_pipeline(int32_t on) {
   return 0;
 }
 
-extern "C" int echo_attention_set_combine(int32_t fused) {
-  if (fused < 0 || fused > 3) return ECHO_EINVAL;
-  if (fused >= 2) g_attn_split_pl = fused == 3;  // diagnostics: 2 = compiler-scheduled split kernel, 3 = pipelined
-  else g_attn_fused_combine = fused;
-  return 0;
-}
-
 extern "C" int echo_attention_set_split(int32_t nsplit) {
   if (nsplit < -1 || nsplit > 16) return ECHO_EINVAL;
   g_attn_split_override = nsplit;
@@ -1740,15 +1291,9 @@ extern "C" int echo_attention_split(const EchoAttnArgs* a, int32_t nsplit, void*
   if (nsplit > 16) return ECHO_EINVAL;
   if (!ws || (uintptr_t)ws % 16 || ws_bytes < echo_attention_split_ws_bytes(a, nsplit)) return ECHO_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  int* cnt = attn_counters(s, attn_grid(a, 128));
-  if (g_attn_pl && !cnt && !any_causal(a) && g_attn_split_pl)  // the pipelined split kernel (bitwise the same partials)
-    hipLaunchKernelGGL((attn_pl_kernel<0, 4, 2, 2, 1>), dim3(attn_grid(a, 128) * nsplit), dim3(256), 0, s, *a,
-                       (float*)ws, (int)nsplit);
-  else
-    hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 0, 1>), dim3(attn_grid(a, 128) * nsplit), dim3(256), 0, s, *a,
-                       (float*)ws, (int)nsplit, cnt);
+  hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 0, 1>), dim3(attn_grid(a, 128) * nsplit), dim3(256), 0, s, *a,
+                     (float*)ws, (int)nsplit);
   ECHO_LAUNCH_CHECK();
-  if (cnt) return 0;  // merged by each item's last workgroup
   hipLaunchKernelGGL(attn_combine_kernel, dim3(a->rows * a->heads * ((a->n_q + 15) / 16)), dim3(256), 0, s, *a,
                      (const float*)ws, (int)nsplit);
   ECHO_LAUNCH_CHECK();

@@ -35,8 +35,7 @@ struct Epi {
   // ECHO_EPI_HEADNORM
   const void* hn_w; int64_t hn_w_stride; const float* hn_rope;
   int hn_heads, hn_nblk, hn_rope_heads, hn_seq_len, hn_pos0, hn_pos_mult; float hn_eps;
-  int stagger;  // pp2 diagnostic (tile 14): first-round start delay per CU group, 10 ns ticks;
-                // persistent kernel: group-M height (set by launch_ps_ek)
+  int gm;  // persistent 256x256 kernel: group-M height (set by launch_ps_ek; tile 18 + diag key 1: override)
   const void* act_alpha;        // ECHO_ACT_SNAKE
   int conv_c, conv_taps, conv_dil;  // causal-conv A addressing (echo_hip.h)
   // RESID + the next AdaLN (EchoGemmArgs.mod_*; the split-K finish kernel only)
@@ -999,13 +998,6 @@ gemm_bf16_pp2_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   for (int c = 0; c < 4; ++c) dma(c, 0);
   if (nk > 1) {
     dma(0, 1); dma(1, 1); dma(2, 1);
-    if (ep.stagger > 0 && bid < 256) {
-      // diagnostic: first-round workgroups start in 8 groups per XCD, `stagger` ticks apart, so
-      // the tile rounds (and their epilogue store bursts) are spread in time
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      const uint64_t until = t0 + (uint64_t)(((bid >> 3) & 7) * ep.stagger);
-      while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(2);
-    }
     vm_wait_n<8>();
   } else {
     vm_wait_n<2>();
@@ -1093,7 +1085,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, uint32_t 
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-template <int EK, int CP = 0>  // CP: cache policy bits of the epilogue stores (2 = nt; diagnostic)
+template <int EK>
 __global__ void __launch_bounds__(512)
 gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
                     const bf16_t* __restrict__ W, int64_t ldw, int64_t sW,
@@ -1118,9 +1110,8 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   W += z * sW;
   const int ntl = tiles_m * tiles_n;
   const int q8 = ntl >> 3, r8 = ntl & 7;
-  // group-M height, chosen on the host (launch_ps_ek; tile 18: diagnostic override) and passed in
-  // ep.stagger, which this kernel does not otherwise use
-  const int GM = ep.stagger > 0 ? ep.stagger : 8;
+  // group-M height, chosen on the host (launch_ps_ek; tile 18: diagnostic override)
+  const int GM = ep.gm > 0 ? ep.gm : 8;
   // tile t -> origin: gemm_bf16_pp2_kernel's XCD-chunked group-M order with t in place of the
   // block id (t = blockIdx.x + r * gridDim.x keeps t & 7 = the XCD when gridDim.x % 8 == 0)
   auto origin = [&](int t, int& m0, int& n0) __attribute__((always_inline)) {
@@ -1435,7 +1426,7 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
         const uint32_t off = (uint32_t)(((mb + ii * 16) * ldc + nb) * 2);
 #pragma unroll
         for (int p = 0; p < FN / 2; ++p)
-          __builtin_amdgcn_raw_buffer_store_b128(swap_pair(hp[ii][2 * p], hp[ii][2 * p + 1]), crs, off + p * 64, 0, CP);
+          __builtin_amdgcn_raw_buffer_store_b128(swap_pair(hp[ii][2 * p], hp[ii][2 * p + 1]), crs, off + p * 64, 0, 0);
       }
     } else if constexpr (EK == EK_SWIGLU) {
       // gate/up column blocks interleaved by 16 (j = 2jj gate, 2jj+1 up), as gemm_epilogue; the
@@ -1455,7 +1446,7 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
           q[jj] = make_uint2(pack2bf(u[0], u[1]), pack2bf(u[2], u[3]));
         }
         const u32x4 o = swap_pair(q[0], q[1]);
-        __builtin_amdgcn_raw_buffer_store_b128(o, crs, (uint32_t)(((mb + ii * 16) * ldc + nbo) * 2), 0, CP);
+        __builtin_amdgcn_raw_buffer_store_b128(o, crs, (uint32_t)(((mb + ii * 16) * ldc + nbo) * 2), 0, 0);
       }
     } else {
 #pragma unroll
@@ -1486,7 +1477,7 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
               o[w] = pack2bf(v0, v1);
             }
           }
-          __builtin_amdgcn_raw_buffer_store_b128(o, crs, off + p * 64, 0, CP);
+          __builtin_amdgcn_raw_buffer_store_b128(o, crs, off + p * 64, 0, 0);
         }
       }
     }
@@ -1540,7 +1531,7 @@ struct T320Args {
   Epi ep;
 };
 
-template <int EK, int SP = 1, int PER = 0, int CP = 0>  // CP: cache policy of the epilogue stores (16 = sc1; A/B)
+template <int EK, int SP = 1, int PER = 0>
 __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
   static_assert(EK == EK_RESID || EK == EK_SWIGLU || EK == EK_HEADNORM, "320-row tiles: residual / SwiGLU / head norm");
   static_assert(!(PER && SP), "persistent form: 2 / 7 DMA split only");
@@ -1870,7 +1861,7 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
         const uint32_t off = (uint32_t)((m * ldc + nb) * 2);
 #pragma unroll
         for (int p = 0; p < FN / 2; ++p)
-          __builtin_amdgcn_raw_buffer_store_b128(swap_pair(hp[2 * p], hp[2 * p + 1]), crs, off + p * 64, 0, CP);
+          __builtin_amdgcn_raw_buffer_store_b128(swap_pair(hp[2 * p], hp[2 * p + 1]), crs, off + p * 64, 0, 0);
         // PER: one row fragment at a time (hipcc otherwise hoists the next fragments' table loads and spills)
         if constexpr (PER) __builtin_amdgcn_sched_barrier(0);
       }
@@ -1894,7 +1885,7 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
             q[jj] = make_uint2(pack2bf(u[0], u[1]), pack2bf(u[2], u[3]));
           }
           __builtin_amdgcn_raw_buffer_store_b128(swap_pair(q[0], q[1]), crs,
-                                                 (uint32_t)(((mb + ii * 16) * ldc + nbo + p * 32) * 2), 0, CP);
+                                                 (uint32_t)(((mb + ii * 16) * ldc + nbo + p * 32) * 2), 0, 0);
         }
       }
     } else {
@@ -1932,7 +1923,7 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
             v1 = bf2f(xr[ii & 1][p][w] >> 16) + v1;
             o[w] = pack2bf(v0, v1);
           }
-          __builtin_amdgcn_raw_buffer_store_b128(o, crs, off + p * 64, 0, CP);
+          __builtin_amdgcn_raw_buffer_store_b128(o, crs, off + p * 64, 0, 0);
         }
       }
     }
@@ -2246,7 +2237,7 @@ int launch_pp2_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 
 int g_num_cus = 0;  // persistent grid size (hipDeviceProp multiProcessorCount, queried once)
 
-template <int EK, int CP = 0>
+template <int EK>
 int launch_ps_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   const int tm = (a->M + 255) / 256, tn = (a->N + 255) / 256;
   if (g_num_cus == 0) {
@@ -2262,8 +2253,8 @@ int launch_ps_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   // 2-6 % slower on QKVG/W13; on the N = 2048 residual GEMMs 4 was within +-2 % of 8 in either
   // direction across two boxes (Wo 245 vs 252 / 235 vs 229 us, W2 591 vs 604 / 579 vs 587 us)
   Epi e = ep;
-  if (e.stagger <= 0) e.stagger = 8;
-  hipLaunchKernelGGL((gemm_bf16_ps_kernel<EK, CP>), dim3(grid, a->batch), dim3(512), 0, s, (const bf16_t*)a->A,
+  if (e.gm <= 0) e.gm = 8;
+  hipLaunchKernelGGL((gemm_bf16_ps_kernel<EK>), dim3(grid, a->batch), dim3(512), 0, s, (const bf16_t*)a->A,
                      a->lda, a->stride_a, (const bf16_t*)a->W, a->ldw, a->stride_w, a->C, a->ldc, a->stride_c,
                      a->M, a->N, a->K, tm, tn, e);
   ECHO_LAUNCH_CHECK();
@@ -2307,14 +2298,13 @@ bool ps_ok(const EchoGemmArgs* a, int ek) {
   return true;
 }
 
-template <int CP = 0>
 int launch_ps(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   switch (ek_of(a)) {
-    case EK_STORE: return launch_ps_ek<EK_STORE, CP>(a, ep, s);
-    case EK_SWIGLU: return launch_ps_ek<EK_SWIGLU, CP>(a, ep, s);
-    case EK_RESID: return launch_ps_ek<EK_RESID, CP>(a, ep, s);
-    case EK_BIAS: return launch_ps_ek<EK_BIAS, CP>(a, ep, s);
-    case EK_HEADNORM: return launch_ps_ek<EK_HEADNORM, CP>(a, ep, s);
+    case EK_STORE: return launch_ps_ek<EK_STORE>(a, ep, s);
+    case EK_SWIGLU: return launch_ps_ek<EK_SWIGLU>(a, ep, s);
+    case EK_RESID: return launch_ps_ek<EK_RESID>(a, ep, s);
+    case EK_BIAS: return launch_ps_ek<EK_BIAS>(a, ep, s);
+    case EK_HEADNORM: return launch_ps_ek<EK_HEADNORM>(a, ep, s);
     default: return ECHO_EINVAL;
   }
 }
@@ -2370,10 +2360,8 @@ bool t320_ok(const EchoGemmArgs* a) {
   return true;
 }
 
-int g_gemm_t320_np = 0;  // echo_gemm_set_diag key 10: 1 = the non-persistent 320-row kernel (A/B)
-
 // PER = 1: one persistent workgroup per CU (grid = min(tiles, CUs rounded down to a multiple of 8))
-template <int SP, int PER, int CP = 0>
+template <int SP, int PER>
 int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   const int tm = a->M / 320, tn = a->N / 256;
   int grid = tm * tn;
@@ -2383,27 +2371,26 @@ int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   }
   const T320Args ta{(const bf16_t*)a->A, a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep};
   if (ek_of(a) == EK_SWIGLU)
-    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_SWIGLU, SP, PER, CP>), dim3(grid), dim3(512), 0, s, ta);
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_SWIGLU, SP, PER>), dim3(grid), dim3(512), 0, s, ta);
   else if (ek_of(a) == EK_HEADNORM)
-    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_HEADNORM, SP, PER, CP>), dim3(grid), dim3(512), 0, s, ta);
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_HEADNORM, SP, PER>), dim3(grid), dim3(512), 0, s, ta);
   else
-    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_RESID, SP, PER, CP>), dim3(grid), dim3(512), 0, s, ta);
+    hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_RESID, SP, PER>), dim3(grid), dim3(512), 0, s, ta);
   ECHO_LAUNCH_CHECK();
   return 0;
 }
 // production 320-row launch: the persistent form for SwiGLU launches of at least 4 tiles per CU (W13: 15 / 5
 // tiles per CU at M = 30720 / 10240, -2.5 / -3 %, C3 +0.8 %; profiles/r3_t320_persistent.txt, r3s2_ab_t320p.txt)
-// unless diag key 10 asks for one tile per workgroup. One tile per workgroup for the blockwise W13 launch
+// (tile 22 forces one tile per workgroup, 23 the persistent form). One tile per workgroup for the blockwise W13 launch
 // (M = 7680: 2 tiles per CU, C5 -0.4 % when persistent) and the gated residual (3 / 1 tiles per CU, K = 5888 for
 // W2: no measurable gain). The head-norm epilogue's persistent form (spill-free since round 4: norm weights
 // and RoPE rows read at the use) from 8 tiles per CU: QKVG M = 30720 (12 per CU) 764.6 -> 753.0 us, M = 10240
 // (4 per CU) 258.5 vs 258.7 (profiles/r4_t320_headnorm_persistent.txt).
-template <int CP = 0>
 int launch_t320(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   const int64_t tiles = (int64_t)(a->M / 320) * (a->N / 256), cus = cu_count_cached();
   const int ek = ek_of(a);
-  const bool per = !g_gemm_t320_np && ((ek == EK_SWIGLU && tiles >= 4 * cus) || (ek == EK_HEADNORM && tiles >= 8 * cus));
-  return per ? launch_t320_sp<0, 1, CP>(a, ep, s) : launch_t320_sp<0, 0, CP>(a, ep, s);
+  const bool per = ((ek == EK_SWIGLU && tiles >= 4 * cus) || (ek == EK_HEADNORM && tiles >= 8 * cus));
+  return per ? launch_t320_sp<0, 1>(a, ep, s) : launch_t320_sp<0, 0>(a, ep, s);
 }
 
 // auto pick between 320x256 and 256x256 tiles by whole rounds of the CUs: a 320-row tile does 1.25x the work
@@ -2441,7 +2428,7 @@ int t320_col_split(const EchoGemmArgs* a, int cus) {
 
 int g_gemm_t320 = 0;  // echo_gemm_set_diag key 7: 320-row tiles in the auto pick: 0 = when they need fewer
                       // tile-rounds x 1.2 (t320_pays), 1 = never, 2 = whenever at least one round (A/B)
-int g_gemm_stagger = 0;  // echo_gemm_set_diag key 1
+int g_gemm_gm = 0;  // echo_gemm_set_diag key 1: group-M height of tile 18 (A/B)
 int g_gemm_no_rowsplit = 0;  // key 3: no row-tail split of 256x256 launches (A/B)
 int g_gemm_no_ps = 0;        // key 4: the 2-phase kernel instead of the persistent one (A/B)
 int g_gemm_no_colsplit = 0;  // key 8: no column split of 320-row launches (t320_col_split; A/B)
@@ -2632,7 +2619,7 @@ extern int g_adaln_blocks;  // elementwise.hip
 
 extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   if (value < 0) return ECHO_EINVAL;
-  if (key == 1) g_gemm_stagger = value;
+  if (key == 1) g_gemm_gm = value;
   else if (key == 2) g_gemm_ns3 = value != 0;
   else if (key == 3) g_gemm_no_rowsplit = value != 0;
   else if (key == 4) g_gemm_no_ps = value != 0;
@@ -2641,7 +2628,6 @@ extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   else if (key == 7) { if (value > 2) return ECHO_EINVAL; g_gemm_t320 = value; }
   else if (key == 8) g_gemm_no_colsplit = value != 0;
   else if (key == 9) g_adaln_blocks = value;
-  else if (key == 10) g_gemm_t320_np = value != 0;
   else if (key == 11) g_gemm_no_splitk = value != 0;
   else if (key == 12) g_gemm_no_sk = value != 0;
   else return ECHO_EINVAL;
@@ -2759,7 +2745,7 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
         return launch_sk_cfg(a, ep, c, S, nullptr, (hipStream_t)stream);
     }
   }
-  if (a->tile == 14 || a->tile == 18) ep.stagger = g_gemm_stagger;
+  if (a->tile == 18) ep.gm = g_gemm_gm;
   if (a->tile == 15) ep.epi = 99;  // diagnostic: no epilogue
   int t = a->tile > 0 ? a->tile : pick_tile(a->M, a->N, a->K, a->batch);
   // 256x256 tiles run the persistent 2-phase kernel where its register epilogue applies, else the
@@ -2767,8 +2753,8 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
   if (a->tile == 0 && t == 1) t = (a->dtype == ECHO_BF16 && ps_ok(a, ek_of(a)) && !g_gemm_no_ps) ? 16 : 13;
   // fused on the persistent kernel (t 16/17/18, N % 256 == 0, via ps_ok) or the 2-phase one (t 13)
   const bool hn_fused = a->dtype == ECHO_BF16 && ((t == 13 && a->N % 128 == 0) ||
-                                                   ((t == 16 || t == 17 || t == 18 || t == 25) && ps_ok(a, EK_HEADNORM)) ||
-                                                   ((t >= 20 && t <= 24) && t320_ok(a)));
+                                                   ((t == 16 || t == 18) && ps_ok(a, EK_HEADNORM)) ||
+                                                   ((t >= 20 && t <= 23) && t320_ok(a)));
   if (headnorm && !hn_fused) {
     // not fused for this shape / dtype: plain store, then the standalone kernel (same results)
     EchoGemmArgs b = *a;
@@ -2803,8 +2789,6 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
   if (a->tile == 21) return t320_ok(a) ? launch_t320_sp<1, 0>(a, ep, s) : ECHO_EINVAL;  // 4 / 5 DMA split (A/B)
   if (a->tile == 22) return t320_ok(a) ? launch_t320_sp<0, 0>(a, ep, s) : ECHO_EINVAL;  // one tile per workgroup
   if (a->tile == 23) return t320_ok(a) ? launch_t320_sp<0, 1>(a, ep, s) : ECHO_EINVAL;  // persistent
-  if (a->tile == 24) return t320_ok(a) ? launch_t320<16>(a, ep, s) : ECHO_EINVAL;  // sc1 (L2-bypassing) stores, A/B
-  if (a->tile == 25) return (a->dtype == ECHO_BF16 && ps_ok(a, ek_of(a))) ? launch_ps<16>(a, ep, s) : ECHO_EINVAL;
   if (a->tile == 0 && g_gemm_t320 == 0 && !g_gemm_no_colsplit && a->batch == 1 && !headnorm && t320_ok(a)) {
     const int c1 = t320_col_split(a, cu_count_cached());
     if (c1 > 0) {
@@ -2857,9 +2841,8 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
     case 10: return launch_pp<4>(a, ep, s);
     case 11: return launch_pp<8>(a, ep, s);
     case 12: return launch_pp<11>(a, ep, s);
-    case 13: case 14: case 15: return launch_pp2(a, ep, s);
+    case 13: case 15: return launch_pp2(a, ep, s);
     case 16: return ps_ok(a, ek_of(a)) ? launch_ps(a, ep, s) : launch_pp2(a, ep, s);
-    case 17: return ps_ok(a, ek_of(a)) ? launch_ps<2>(a, ep, s) : launch_pp2(a, ep, s);
     case 18: return ps_ok(a, ek_of(a)) ? launch_ps(a, ep, s) : ECHO_EINVAL;  // group-M override (diag key 1)
     default: return ECHO_EINVAL;
   }

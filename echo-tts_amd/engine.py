@@ -456,9 +456,9 @@ def _split_sizes(B: int, N: int) -> Optional[Tuple[int, int]]:
 
 
 def plan_key(B, N, Tc, Pc, sched: Schedule, kv_scale, kv_max_layers):
-    # the split policy (ops.policy_rows) is part of the key: a captured graph holds the split-K / split-KV
-    # choices made under it
-    return (B, N, Tc, Pc, sched, kv_scale, kv_max_layers, ops.current_policy_rows())
+    # the split policy (ops.policy_rows) and the split / kernel switches (ops.attention_split, gemm_no_splitk,
+    # attention_pipeline) are part of the key: a captured graph holds the choices made under them
+    return (B, N, Tc, Pc, sched, kv_scale, kv_max_layers, ops.current_split_state())
 
 
 def _cached(model: EchoDiTHip, key, make):

@@ -145,31 +145,51 @@ def attention(q: Tensor, segments: Sequence[Segment], out: Optional[Tensor] = No
     return out
 
 
-@contextlib.contextmanager
-def attention_split(nsplit: int):
-    """Force the split-KV count of `attention` inside the block (1 = never split; tests and
-    tools/bench_attn.py). Outside it the host policy (echo_attention_pick_split) decides."""
-    rc = lib().echo_attention_set_split(int(nsplit))
+# Process-global library switches that change which kernels (and so which summation orders) a launch runs.
+# Their current values are kept here so that context managers restore what they replaced (nested use) and a
+# captured plan can be keyed on them (engine.plan_key via current_split_state()).
+_KNOBS = {"attention_split": -1, "gemm_no_splitk": 0, "attention_pipeline": 1}
+
+
+def _set_knob(name: str, value: int) -> None:
+    if name == "attention_split":
+        rc = lib().echo_attention_set_split(int(value))
+    elif name == "gemm_no_splitk":
+        rc = lib().echo_gemm_set_diag(11, int(value))
+    else:
+        rc = lib().echo_attention_set_pipeline(int(value))
     if rc:
-        raise RuntimeError(f"echo_attention_set_split({nsplit}) failed: {rc}")
+        raise RuntimeError(f"{name}({value}) refused by libecho_hip: {rc}")
+    _KNOBS[name] = int(value)
+
+
+@contextlib.contextmanager
+def _knob(name: str, value: int):
+    prev = _KNOBS[name]
+    _set_knob(name, value)
     try:
         yield
     finally:
-        lib().echo_attention_set_split(-1)
+        _set_knob(name, prev)
 
 
-@contextlib.contextmanager
+def attention_split(nsplit: int):
+    """Force the split-KV count of `attention` inside the block (1 = never split; tests and
+    tools/bench_attn.py). Outside it the host policy (echo_attention_pick_split) decides."""
+    return _knob("attention_split", nsplit)
+
+
 def gemm_no_splitk():
     """Inside the block no GEMM splits K (echo_gemm_set_diag key 11): every launch sums K in the one
     order all unsplit kernels share, so B = 1 rows equal B = 16 rows bitwise (tests). Outside it the
     small-M plan may split K of under-filled launches (echo_gemm_ws)."""
-    rc = lib().echo_gemm_set_diag(11, 1)
-    if rc:
-        raise RuntimeError(f"echo_gemm_set_diag(11, 1) failed: {rc}")
-    try:
-        yield
-    finally:
-        lib().echo_gemm_set_diag(11, 0)
+    return _knob("gemm_no_splitk", 1)
+
+
+def attention_pipeline(on: bool):
+    """Route non-causal bf16 attention launches to the asm-owned pipelined kernel (True, the default)
+    or to the compiler-scheduled kernel (False) inside the block (A/B tests and measurements)."""
+    return _knob("attention_pipeline", int(bool(on)))
 
 
 @contextlib.contextmanager
@@ -197,35 +217,15 @@ _POLICY = (1, 1)
 
 
 def current_policy_rows() -> Tuple[int, int]:
-    """The (num, den) set by the innermost `policy_rows` block ((1, 1) outside): part of a captured
-    plan's identity, since its graph holds the split choices taken under it."""
+    """The (num, den) set by the innermost `policy_rows` block ((1, 1) outside)."""
     return _POLICY
 
 
-@contextlib.contextmanager
-def attention_combine(fused: bool):
-    """Split-KV launches merge their splits in each item's last workgroup (True) or in the separate combine
-    kernel (False, the default: faster on MI355X) inside the block (A/B tests; bitwise the same)."""
-    rc = lib().echo_attention_set_combine(int(bool(fused)))
-    if rc:
-        raise RuntimeError(f"echo_attention_set_combine({fused}) failed: {rc}")
-    try:
-        yield
-    finally:
-        lib().echo_attention_set_combine(0)
-
-
-@contextlib.contextmanager
-def attention_pipeline(on: bool):
-    """Route non-causal bf16 attention launches to the asm-owned pipelined kernel (True, the default)
-    or to the compiler-scheduled kernel (False) inside the block (A/B tests and measurements)."""
-    rc = lib().echo_attention_set_pipeline(int(bool(on)))
-    if rc:
-        raise RuntimeError(f"echo_attention_set_pipeline({on}) failed: {rc}")
-    try:
-        yield
-    finally:
-        lib().echo_attention_set_pipeline(1)
+def current_split_state() -> Tuple:
+    """Everything process-global that decides the kernels a captured plan holds: the policy rows and the
+    split / kernel-choice switches above. Part of a plan's identity (engine.plan_key), so a graph captured
+    under one state is never replayed under another."""
+    return (_POLICY, tuple(sorted(_KNOBS.items())))
 
 
 def attention_variant(q: Tensor, segments: Sequence[Segment], out: Tensor, gate: Optional[Tensor] = None,

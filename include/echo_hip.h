@@ -111,10 +111,8 @@ int echo_gemm_ws(const EchoGemmArgs* args, void* ws, int64_t ws_bytes, void* str
  * the whole batch (bitwise-equal gathered output). 1 / 1 (default) = decide on the launch's own rows. */
 int echo_set_policy_rows(int32_t num, int32_t den);
 
-/* Diagnostic knobs for tools/bench_gemm.py (not used by the product path). key 1: start delay
- * between the 8 first-round workgroup groups of an XCD for `tile` = 14 (the 256x256 kernel with
- * staggered tile rounds), in 10 ns ticks; also the persistent kernel's group-M height for
- * `tile` = 18. key 2: 0 turns the 3-stage pipeline of the two smallest tile configs off (A/B
+/* Diagnostic knobs for tools/bench_gemm.py (not used by the product path). key 1: the persistent
+ * 256x256 kernel's group-M height for `tile` = 18. key 2: 0 turns the 3-stage pipeline of the two smallest tile configs off (A/B
  * timing; both schedules give bitwise-equal results). key 3: 1 = no row-tail split of auto-picked
  * 256x256 launches; key 4: 1 = the 2-phase kernel instead of the persistent one for auto-picked
  * 256x256 launches; key 5: tile count below which an auto-picked 256x256 launch switches to a
@@ -123,8 +121,8 @@ int echo_set_policy_rows(int32_t num, int32_t den);
  * tile-rounds than 256x256 tiles, 1 = never, 2 = whenever they fill at least one round); key 8: 1 = no
  * column split of auto-picked 320-row launches (W13: 320-row tiles on whole rounds of tile columns, the
  * rest on the persistent 256x256 kernel); key 9: block cap of the wave-per-row AdaLN kernel (0 = 8192);
- * key 10: 1 = one 320-row tile per workgroup instead of the persistent 320-row SwiGLU kernel (`tile` 22 / 23
- * force either form for any epilogue) (A/B timing, tools/bench_streams.py --diag; all bitwise-equal).
+ * (`tile` 22 / 23 force one 320-row tile per workgroup / the persistent 320-row kernel for any epilogue;
+ * A/B timing, all bitwise-equal; key 10 is retired.)
  * key 11: 1 = never split K in echo_gemm_ws (the B = 1 runs that tests compare bitwise with B = 16 rows);
  * key 12: 1 = no small-M kernel in the auto pick (the round-3 small tiles; A/B).
  * `tile` 100 + 10*C + S (C = small-M config 1..16, S = split 1..9) forces a small-M launch (tools/bench_gemm.py). */
@@ -161,7 +159,7 @@ int echo_attention(const EchoAttnArgs* args, void* stream);
 /* Split-KV form of echo_attention for launches that leave most CUs idle (B = 1 sampler steps,
  * blockwise blocks): each (128-query block, row, head) item's key tiles are split over `nsplit`
  * workgroups that store unnormalised partials (O fp32, running max, row sum) into `ws`, and a
- * combine step (each item's last workgroup, or a separate pass: echo_attention_set_combine) merges
+ * combine pass merges
  * them, normalises, gates and stores `out` (same roundings as echo_attention;
  * only the fp32 summation order over keys differs). nsplit <= 1 runs echo_attention.
  * `ws`: device, 16-B aligned, >= echo_attention_split_ws_bytes(args, nsplit) bytes.
@@ -170,13 +168,6 @@ int echo_attention_split(const EchoAttnArgs* args, int32_t nsplit, void* ws, int
 int64_t echo_attention_split_ws_bytes(const EchoAttnArgs* args, int32_t nsplit);
 /* Host policy: the split count echo_attention_split should use for these shapes (1 = none). */
 int32_t echo_attention_pick_split(const EchoAttnArgs* args);
-/* 1: split-KV launches merge their splits in the split kernel itself — the last workgroup of each (row, head,
- * query block) to finish combines the partials (an agent-scope counter per item in a per-device array the
- * library allocates and clears on the first split launch outside stream capture; a launch before that, under
- * capture, uses the combine kernel); bitwise the same. Concurrent split launches on different streams of one
- * device must not use it. 0 (default): the separate combine kernel — measured faster on MI355X.
- * Diagnostics: 2 / 3 = the split kernel on the compiler-scheduled (default) / asm-pipelined tile loop. */
-int echo_attention_set_combine(int32_t fused);
 /* Diagnostics: force the policy's answer (0/1 = never split, 2..16), -1 = back to the policy. */
 int echo_attention_set_split(int32_t nsplit);
 /* Diagnostics: 1 (default) = non-causal bf16 launches run the asm-owned software-pipelined kernel
@@ -331,7 +322,7 @@ const char* echo_version(void);
  * (4: EchoAttnArgs gained the trailing q_batch_mod; 5: EchoGemmArgs gained the mod_* fields of the fused
  * residual + AdaLN). A binding built against an older header must
  * refuse to run: check echo_abi_version() == ECHO_ABI_VERSION and the struct sizes below at load. */
-#define ECHO_ABI_VERSION 5
+#define ECHO_ABI_VERSION 6
 int32_t echo_abi_version(void);
 /* sizeof() of an argument struct as this library was compiled: 0 EchoGemmArgs, 1 EchoAttnArgs,
  * 2 EchoKVSegment, 3 EchoStepArgs, 4 EchoRvqWeights; -1 for an unknown id. */

@@ -240,5 +240,5 @@ def test_gemm_small_m_plan_host_policy(lib):
         assert lib.echo_set_policy_rows(1, 1) == 0
     assert ws(160, 2048, 5888) == 4 * 160 * 2048 * 4
     assert lib.echo_set_policy_rows(1, 2) != 0
-    assert lib.echo_attention_set_combine(4) != 0 and lib.echo_attention_set_combine(-1) != 0
-    assert lib.echo_attention_set_combine(0) == 0 and lib.echo_attention_set_combine(2) == 0
+    assert lib.echo_attention_set_pipeline(3) != 0 and lib.echo_attention_set_pipeline(-1) != 0
+    assert lib.echo_attention_set_pipeline(0) == 0 and lib.echo_attention_set_pipeline(1) == 0

@@ -201,6 +201,43 @@ def test_c5_engine_end_to_end_bf16(m16, c5):
     gate("C5 end-to-end bf16", lat.cpu(), g["bf16.latent"], g["fp32.latent"], 5e-3, floor=traj_floor("c5"))
 
 
+def test_c5_rows_bitwise_equal_b1(m16, c5):
+    """C5 at B = 16 (the bench's driver-timed `c5` leg) through the captured BlockPlan graph: every row is
+    bitwise the B = 1 run of its prompt (unsplit attention, unsplit GEMMs), and row 0 is gated against the
+    reference's C5 run (/root/reference/inference_blockwise.py:14-123). The B = 16 call runs launch shapes no
+    B = 1 test touches: the M = 2560 plain-step residuals on the 160x128 8-wave small-M tiles, the 7680-row
+    320-row / column-split GEMMs and R = 48 attention over [self | latent | text | speaker]."""
+    g, meta = c5
+    B, nb = 16, len(meta["blocks"])
+    ids, tm = SY.text_inputs(B)
+    spk, sm = SY.speaker_inputs(B)
+    assert torch.equal(ids[0], g["text_ids"][0]) and torch.equal(spk[0], g["speaker_latent"][0])
+    gen = torch.Generator().manual_seed(78)
+    blocks = []
+    for j, n in enumerate(meta["blocks"]):
+        nz = torch.randn((B, n, 80), generator=gen)
+        nz[0] = g[f"noise{j}"][0]
+        blocks.append(nz.to(DEV))
+    ids, tm, spk, sm = (t.to(DEV) for t in (ids, tm, spk, sm))
+    kw = _kw(meta)
+
+    def noise_rows(lo, hi):
+        it = iter([b[lo:hi] for b in blocks])
+        return lambda shape: next(it)
+
+    lat16 = blockwise_with_noise(m16, spk, sm, ids, tm, noise_rows(0, B), meta["blocks"], use_graph=True, **kw)
+    lat16 = blockwise_with_noise(m16, spk, sm, ids, tm, noise_rows(0, B), meta["blocks"], use_graph=True, **kw)
+    assert torch.isfinite(lat16).all()
+    with ops.attention_split(1), ops.gemm_no_splitk():
+        for b in range(B):
+            one = blockwise_with_noise(m16, spk[b:b + 1], sm[b:b + 1], ids[b:b + 1], tm[b:b + 1],
+                                       noise_rows(b, b + 1), meta["blocks"], use_graph=False, **kw)
+            assert torch.equal(lat16[b:b + 1], one), b
+    assert nb == 4
+    gate("C5 B=16 row 0 end-to-end bf16", lat16[:1].cpu(), g["bf16.latent"], g["fp32.latent"], 5e-3,
+         floor=traj_floor("c5"))
+
+
 # ------------------------------------------------------------------------------ blockwise continuation
 # inference_blockwise.py:58-65 + its __main__ continuation example: a 317-latent prefix (start_pos not a
 # multiple of 4), one 255-latent block, partial speaker mask, text 203/257, truncation 0.8 and the

@@ -339,7 +339,7 @@ def ref_attention(q, segs, gate, scale, dtype):
     return o
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 6, 7, 8, 9])
 def test_attention_variants_match_production(variant):
     """Diagnostic entry point: every measurement variant computes the production result
     (variant 0 bitwise; the others up to accumulation-order rounding), and the timeline
@@ -436,60 +436,6 @@ def test_attention_split_kv(nsplit, R, n_q):
         ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])  # workspace reuse
     torch.cuda.synchronize()
     split_close(got, ref, ref_attention(qkvg[:, :, 0], segs, qkvg[:, :, 3], 128 ** -0.5, BF))
-
-
-@pytest.mark.parametrize("nsplit", [2, 3, 4, 16])
-@pytest.mark.parametrize("R,n_q", [(1, 640), (3, 160), (1, 37)])
-def test_attention_split_fused_combine_bitwise(nsplit, R, n_q):
-    """The split kernel's fused combine (each item's last workgroup merges the partials, agent-scope counters
-    that reset themselves) is bitwise the separate combine kernel — eager, repeated (counters back at 0
-    after every launch) and replayed from a captured hipGraph."""
-    qkvg, segs = _small_batch_segments(1, R, n_q, H=4, tl_valid=271)
-    ref = torch.full((R, n_q, 4, 128), float("nan"), device=DEV, dtype=BF)
-    with ops.attention_split(nsplit), ops.attention_combine(False):
-        ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
-    got = torch.full_like(ref, float("nan"))
-    with ops.attention_split(nsplit), ops.attention_combine(True):
-        for _ in range(3):
-            got.fill_(float("nan"))
-            ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
-            torch.cuda.synchronize()
-            assert torch.equal(got, ref)
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
-        torch.cuda.current_stream().wait_stream(s)
-        for _ in range(3):
-            got.fill_(float("nan"))
-            g.replay()
-            torch.cuda.synchronize()
-            assert torch.equal(got, ref)
-
-
-@pytest.mark.parametrize("nsplit", [2, 3, 4, 16])
-@pytest.mark.parametrize("R,n_q", [(1, 640), (3, 160), (1, 37)])
-def test_attention_split_pipelined_bitwise(nsplit, R, n_q):
-    """The split kernel on the asm-pipelined tile loop (attn_pl_kernel SP = 1) stores bitwise the partials of
-    the compiler-scheduled split kernel (attn_bf16_kernel SP = 1, production): equal outputs after the
-    combine, incl. splits with no tiles."""
-    lib = L.load()
-    qkvg, segs = _small_batch_segments(1, R, n_q, H=4, tl_valid=271)
-    ref = torch.full((R, n_q, 4, 128), float("nan"), device=DEV, dtype=BF)
-    got = torch.full_like(ref, float("nan"))
-    try:
-        assert lib.echo_attention_set_combine(2) == 0
-        with ops.attention_split(nsplit):
-            ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
-        assert lib.echo_attention_set_combine(3) == 0
-        with ops.attention_split(nsplit):
-            ops.attention(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3])
-    finally:
-        lib.echo_attention_set_combine(2)
-    torch.cuda.synchronize()
-    assert torch.equal(got, ref)
 
 
 @pytest.mark.parametrize("L_", [37, 160, 333])
@@ -596,13 +542,6 @@ def test_attention_pipeline_bitwise(case):
         got.fill_(float("nan"))
         ops.attention(q[:, :, 0], segs, out=got, gate=gate)
     assert torch.equal(got, ref)
-    # deeper K / V rings (variants 26 / 27 / 28 / 29: 3 + 2, 3 + 3, 4 + 4, 2 + 3 slots, counted waits across the
-    # barrier): the same bodies on other LDS slots, bitwise equal
-    for v in (26, 27, 28, 29):
-        got.fill_(float("nan"))
-        ops.attention_variant(q[:, :, 0], segs, out=got, gate=gate, variant=v)
-        torch.cuda.synchronize()
-        assert torch.equal(got, ref), (v, float((got != ref).double().mean()))
     if case in ("one_tile", "one_query", "spikes"):
         close_bf16(ref, ref_attention(q[:, :, 0], segs, gate, 128 ** -0.5, BF))
 
@@ -610,8 +549,8 @@ def test_attention_pipeline_bitwise(case):
 def test_attention_engine_kv_layout():
     """The engine's KV layout: one [B, T, 24, 2, H, 128] buffer per stream, layer = strided view
     (1.4 GB for B=16, T=448): tile base addresses span > 2^31 bytes, so any 32-bit address word
-    handled as signed shows up here. Production kernel vs the pipelined variant (independent tile
-    addressing), and both finite."""
+    handled as signed shows up here. Production (asm-pipelined) kernel vs the compiler-scheduled variant 0
+    (independent tile addressing): bitwise equal, and finite."""
     B, N, H, T, P = 16, 640, 16, 448, 160
     R = 3 * B
     qkvg = torch.randn(R, N, 4, H, 128, device=DEV).to(BF)
@@ -627,15 +566,16 @@ def test_attention_engine_kv_layout():
     ref = torch.empty(R, N, H, 128, device=DEV, dtype=BF)
     ops.attention(qkvg[:, :, 0], segs, out=ref, gate=qkvg[:, :, 3])
     got = torch.full_like(ref, float("nan"))
-    ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=5)
+    ops.attention_variant(qkvg[:, :, 0], segs, out=got, gate=qkvg[:, :, 3], variant=0)
     torch.cuda.synchronize()
-    close_bf16(got, ref.float().cpu())
+    assert torch.isfinite(got.float()).all()
+    assert torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("variant", [5])
+@pytest.mark.parametrize("variant", [3, 8])
 @pytest.mark.parametrize("n", [1, 63, 200, 333])
 def test_attention_variant_causal_segments(variant, n):
-    """Pipelined variant on the blockwise layout: causal latent segment (odd lengths, partial
+    """Register-staged (3) and persistent (8) variants on the blockwise layout: causal latent segment (odd lengths, partial
     tiles, single-tile rows), a prefix segment with per-row lengths incl. 0, and a speaker segment."""
     B, H = 2, 2
     R = 3 * B
@@ -953,7 +893,64 @@ def test_gemm_small_m_split_k(M, N, K, epi):
         close_bf16(auto[:, :nout], rb(ref_linear(a, w)))
 
 
-def test_gemm_small_m_policy_rows():
+def bf16_ulps(got, ref):
+    """Distance in bf16 ulps between two bf16-valued tensors (order-preserving integer map of the bit
+    patterns, so +0 / -0 are 0 apart and consecutive bf16 values 1 apart)."""
+    def key(t):
+        b = t.to(BF).cpu().view(torch.int16).to(torch.int32)
+        return torch.where(b < 0, -(b & 0x7FFF), b)
+    return (key(got) - key(ref)).abs()
+
+
+def _epilogue_ref64(a, w, h, gate, hn, nout, epi):
+    """The epilogue of the reference's modules on an fp64 product, at the reference's bf16 rounding points:
+    STORE round(aWᵀ); SWIGLU round(round(silu(round(a w1ᵀ))) * round(a w3ᵀ)) (model.py:303-308);
+    RESID round(h + round(gate * round(aWᵀ))) (model.py:385, 388); HEADNORM q/k RMSNorm + half RoPE of
+    round(aWᵀ) (model.py:217-232) through the oracle's restatement."""
+    y = ref_linear(a, w).double()
+    if epi == L.EPI_SWIGLU:
+        K = w.shape[1]
+        w12 = w.reshape(-1, 2, 16, K)
+        x1 = rb(ref_linear(a, w12[:, 0].reshape(-1, K)))
+        x3 = rb(ref_linear(a, w12[:, 1].reshape(-1, K)))
+        return rb(rb(torch.nn.functional.silu(x1.double()).float()) * x3)
+    y = rb(y.float())
+    if epi == L.EPI_STORE:
+        return y
+    if epi == L.EPI_RESID:
+        return rb(h[:, :nout].float().cpu() + rb(gate.float().cpu() * y))
+    from oracle import echo_oracle as O
+    H, M = hn.heads, y.shape[0]
+    assert hn.rope_heads == H // 2 and hn.nblk == 2  # _sk_case's decoder layout: q, k normed, half RoPE
+    out = y.clone()
+    pos = (torch.arange(M) % hn.seq_len) + hn.pos0
+    table = O.rope_table(128, 4096)[pos]
+    for blk in range(2):  # bf16 tensors: O.rms / O.rotate round where the reference's bf16 modules do
+        v = y[:, blk * H * 128:(blk + 1) * H * 128].to(BF).reshape(1, M, H, 128)
+        r = O.rotate_half_heads(O.rms(v, hn.w.reshape(2, H, 128)[blk].cpu(), hn.eps), table)
+        out[:, blk * H * 128:(blk + 1) * H * 128] = r.reshape(M, H * 128).float()
+    return out
+
+
+@pytest.mark.parametrize("M,N,K", [(640, 2048, 5888), (480, 2048, 2048), (160, 11776, 2048), (333, 1024, 512)])
+@pytest.mark.parametrize("epi", [L.EPI_STORE, L.EPI_SWIGLU, L.EPI_RESID, L.EPI_HEADNORM])
+def test_gemm_split_k_epilogues_vs_fp64(M, N, K, epi):
+    """Each epilogue of the split-K finish kernel (gemm_splitk_finish_kernel: SwiGLU, gated residual, q/k head
+    norm + RoPE, plain store) against the same epilogue computed from an fp64 product with the reference's
+    rounding points — not against another HIP kernel. Gate: the bf16 output-rounding bound, <= 1 bf16 ulp on
+    >= 99.9 % of the elements (the fp32 partial sums may round the other way at a bf16 midpoint), for every
+    forced split S = 2 / 3 / 8 of the 128x128 config and the auto plan."""
+    a, w, h, gate, hn, nout = _sk_case(M, N, K, epi)
+    ref = _epilogue_ref64(a, w, h, gate, hn, nout, epi)
+    for tile in (112, 113, 118, 162, 0):
+        if tile and K // 64 < tile % 10:
+            continue
+        got = _sk_run(a, w, h, gate, hn, nout, epi, tile)[:, :nout]
+        d = bf16_ulps(got.float(), ref)
+        frac = float((d <= 1).double().mean())
+        print(f"[split-K epi {epi} M={M} N={N} K={K} tile {tile}] <=1 ulp {frac:.5f}  max {int(d.max())} ulp")
+        assert frac >= 0.999, (tile, frac)
+
     """echo_set_policy_rows: the split decision for a launch of M rows taken as for M * num / den rows —
     a rank holding 1 of 8 prompts splits K exactly like the one-process run of 8 prompts (here: not at
     all), so its rows are bitwise those of that run."""

@@ -38,9 +38,6 @@ def main():
     ap.add_argument("--splits", default=None,
                     help="comma list of forced split-KV counts (1 = unsplit) for the production op: interleaved "
                          "rounds, median per count")
-    ap.add_argument("--split-kernels", action="store_true",
-                    help="with --splits: each count on the compiler-scheduled (c) and asm-pipelined (p) split "
-                         "kernel (echo_attention_set_combine 2 / 3), interleaved")
     args = ap.parse_args()
     dev = "cuda"
     B, N, H, T, P = args.batch, args.nq, 16, 448, 160
@@ -83,18 +80,13 @@ def main():
             if args.splits:
                 counts = [int(v) for v in args.splits.split(",")]
                 f = lambda: ops.attention(qkvg[:, :, 0], segs, out=out, gate=qkvg[:, :, 3])  # noqa: E731
-                kinds = (("c", 2), ("p", 3)) if args.split_kernels else (("", 3),)
-                tm = {(c, kn): [] for c in counts for kn, _ in kinds}
+                tm = {c: [] for c in counts}
                 for _ in range(7):
                     for c in counts:
-                        for kn, mode in kinds:
-                            ops.lib().echo_attention_set_combine(mode)
-                            with ops.attention_split(c):
-                                f()
-                                tm[(c, kn)].append(timeit(f, rounds=1))
-                ops.lib().echo_attention_set_combine(2)
-                ops.lib().echo_attention_set_split(-1)
-                line = "  ".join(f"s{c}{kn} {sorted(v)[3] * 1e3:7.1f}" for (c, kn), v in tm.items())
+                        with ops.attention_split(c):
+                            f()
+                            tm[c].append(timeit(f, rounds=1))
+                line = "  ".join(f"s{c} {sorted(v)[3] * 1e3:7.1f}" for c, v in tm.items())
                 print(f"R={R:3d} {name:10s} us by split: {line}", flush=True)
                 continue
             if args.variant is None and not args.ablation:

@@ -71,11 +71,11 @@ def main():
     ap.add_argument("--pad-c", type=int, default=0, help="row stride of the output = N + pad (elements)")
     ap.add_argument("--no-ns3", action="store_true", help="2-stage pipeline for the small tiles (A/B)")
     ap.add_argument("--bias", action="store_true", help="add a bias vector (generic epilogue kind)")
-    ap.add_argument("--stagger", type=int, default=0, help="tile 14: first-round group delay (10 ns ticks)")
+    ap.add_argument("--group-m", type=int, default=0, help="tile 18: group-M height of the persistent 256x256 kernel")
     ap.add_argument("--wcopies", type=int, default=1, help="rotate over this many weight copies (HBM streaming)")
     args = ap.parse_args()
-    if args.stagger:
-        assert L.load().echo_gemm_set_diag(1, args.stagger) == 0
+    if args.group_m:
+        assert L.load().echo_gemm_set_diag(1, args.group_m) == 0
     if args.no_ns3:
         assert L.load().echo_gemm_set_diag(2, 0) == 0
     shapes = SHAPES

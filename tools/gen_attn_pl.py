@@ -12,8 +12,7 @@ attn_pl_kernel (attention.hip) caps the compiler at 96 VGPRs (amdgpu_num_vgpr) a
     v240 .. v255   V^T fragment ring, 4 slots of 4 registers (2 transposed b64 reads each)
 
 The LDS ring slot of the K / V tile a body reads is a literal of the body (pl_x_<buffer>_<K slot>,
-pl_y_<buffer>_<V slot>, up to MAX_SLOTS slots of 16 KiB each; pl_x_cs<C, S> etc. dispatch at compile time),
-so attn_pl_kernel<.., NK, NV> can keep NK K tiles and NV V tiles in its LDS ring.
+pl_y_<buffer>_<V slot>, MAX_SLOTS slots of 16 KiB each; pl_x_cs<C, S> etc. dispatch at compile time).
 
 Each function below is ONE asm statement over those registers, so the compiler never sees (and never
 copies, splits or spills) the loop state; it keeps only addresses, Q and the softmax scalars. The math and
@@ -212,7 +211,7 @@ KIN = [f"[ka{d}] \"v\"(ka[{d}])" for d in range(8)]
 VIN = [f"[va{d}] \"v\"(va[{d}])" for d in range(8)]
 
 
-MAX_SLOTS = 4  # K / V ring slots addressable by the bodies (immediate LDS offsets stay < 64 KiB)
+MAX_SLOTS = 2  # K / V ring slots addressable by the bodies (the 2 + 2 ring of attn_pl_kernel)
 
 
 def gen():
