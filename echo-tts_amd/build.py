@@ -20,7 +20,7 @@ OUT = os.path.join(PKG, "libecho_hip.so")
 TORCH_OUT = os.path.join(PKG, "libecho_torch.so")  # TORCH_LIBRARY(echo_hip) registration over the C ABI
 OBJ = os.path.join(PKG, "build")
 SOURCES = ["gemm.hip", "attention.hip", "elementwise.hip", "codec.hip"]
-HEADERS = [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "attn_pl.inc"), os.path.join(REPO, "include", "echo_hip.h")]
+HEADERS = [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "attn_pl.inc"), os.path.join(CSRC, "attn_w64.inc"), os.path.join(REPO, "include", "echo_hip.h")]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
          "-Wno-unused-result"]
 

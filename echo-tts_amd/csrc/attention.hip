@@ -925,6 +925,269 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
     attn_store_rows(v4, (bf16_t*)a.out + row * a.o_ld_batch + qw * a.o_ld_tok + head * 128, nv, a.o_ld_tok, lane);
   }
 }
+
+// ----------------------------------------------------------------------------- one wave per SIMD, 64 rows
+// attn_w64_kernel: the structure of cdna_hip_programming.md's "4-wave, one-wave-per-SIMD" attention: each wave
+// owns 64 queries (q blocks A = qw .. qw+31, B = qw+32 .. qw+63 of the item's 64 NW) and the whole 512-register
+// file (map: tools/gen_attn_w64.py), so every K / V^T fragment read from LDS feeds two MFMAs. NW = 4: one
+// 256-query workgroup per CU (each K / V tile staged once for 256 queries: half attn_pl_kernel's LDS-DMA per
+// query); NW = 2: two 128-query workgroups per CU. 80 KiB of LDS per workgroup: a 3-slot K ring, a 2-slot V ring. The tile bodies (attn_w64.inc) software-pipeline
+// each wave on its own: X(t) = softmax(t) || QK(t+1) with the DMA of V(t+1) and K(t+3) in its MFMA gaps,
+// Y(t) = PV(t) || row max(t+1). Per 32-query block the math, its order and every rounding are
+// attn_bf16_kernel<0, 4, 2>'s (the deferred-max decision is taken per block, as there): bitwise equal.
+// Non-causal launches only. ABL (timing ablations, results wrong): 1 = no DMA in the tile loop, 8 = no end-of-tile
+// DMA wait (the barrier stays), 16 = no tile loop.
+#include "attn_w64.inc"
+
+template <int ABL, int NW>
+__global__ void __launch_bounds__(64 * NW, 1) __attribute__((amdgpu_num_vgpr(128))) attn_w64_kernel(EchoAttnArgs a_arg) {
+  static_assert(NW == 2 || NW == 4, "2 or 4 waves");
+  using WB = std::conditional_t<NW == 2, W2, W4>;
+  constexpr int QB = 64 * NW, KTT = KT;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[5 * KT * 128];  // K slots 0-2 | V slots 0-1 (80 KiB)
+  using KArgs = const __attribute__((address_space(4))) EchoAttnArgs;
+  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  (void)a_arg;
+  const int nqb = (a.n_q + QB - 1) / QB;
+  const int L = remap_xcd(blockIdx.x, gridDim.x);
+  const int qb = L % nqb;
+  const int Lr = L / nqb;  // rows fastest (see attn_bf16_kernel)
+  const int row = Lr % a.rows, head = Lr / a.rows;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h2 = lane >> 5, ql = lane & 31;
+  const int q0 = qb * QB;
+  const int qw = q0 + 64 * w;  // q block A = qw .. qw + 31, B = qw + 32 .. qw + 63 (rows past n_q: clamped loads)
+  {
+    const int qca = min(qw + ql, a.n_q - 1), qcb = min(qw + 32 + ql, a.n_q - 1);
+    const bf16_t* qbase = (const bf16_t*)a.q + ECHO_QROW(a, row) * a.q_ld_batch + head * 128;
+    WB::load_q((uint32_t)(((int64_t)qca * a.q_ld_tok + 8 * h2) * 2), (uint32_t)(((int64_t)qcb * a.q_ld_tok + 8 * h2) * 2),
+             qbase);
+  }
+
+  ECHO_SEG_TABLE()
+  ECHO_CURSOR_ADVANCE()
+  Cursor kc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // K DMA (3 tiles ahead of the QK)
+  Cursor vc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // V DMA (1 tile ahead of the PV)
+  Cursor mc{-1, 0, 0, 0, 0, 0, nullptr, nullptr};  // the tile whose scores are masked / maxed
+
+  // LDS-DMA lane terms: piece i of the wave covers tile rows 8 i + r0 (r0 = 4 w + lane / 16), its lane reads the
+  // source chunk (lane % 16) ^ swz(row) (cx0 / cx1: even / odd i), into the wave's 1 KiB of the piece's 2 KiB
+  const int dr = lane >> 4, dp = lane & 15;
+  const uint32_t r0 = (uint32_t)(4 * w + dr);
+  const uint32_t cx0 = (uint32_t)((dp ^ ((dr << 2) | w)) * 16), cx1 = (uint32_t)((dp ^ ((dr << 2) | (2 + w))) * 16);
+  const uint32_t lbase = lds_addr_of(lds);
+  const uint32_t lw = __builtin_amdgcn_readfirstlane(lbase + (uint32_t)w * 1024u);
+  struct Dma {
+    const void* base;
+    uint32_t last, ld2;
+  };
+  auto next_dma = [&](Cursor& c, int part) __attribute__((always_inline)) {
+    advance(c);
+    Dma d;
+    d.base = (part ? c.vb : c.kb) + (int64_t)c.t0 * c.ld;
+    d.last = (uint32_t)(c.kend - 1 - c.t0);
+    d.ld2 = (uint32_t)c.ld * 2u;
+    return d;
+  };
+
+  // per-lane LDS byte addresses of the fragment reads (slot / sub-tile offsets are immediates of the bodies)
+  uint32_t ka[8], va[8];
+#pragma unroll
+  for (int ds = 0; ds < 8; ++ds) ka[ds] = lbase + (uint32_t)(ql * 128 + (((2 * ds + h2) ^ swz(ql)) * 8)) * 2u;
+  {
+    const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+    const int rr0 = 4 * h2 + q4, rr1 = rr0 + 8;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int ch = 4 * dt + 2 * (g & 1) + (p4 >> 1);
+      va[2 * dt] = lbase + 3u * KT * 128 * 2 + (uint32_t)(rr0 * 128 + ((ch ^ swz(rr0)) * 8) + (p4 & 1) * 4) * 2u;
+      va[2 * dt + 1] = lbase + 3u * KT * 128 * 2 + (uint32_t)(rr1 * 128 + ((ch ^ swz(rr1)) * 8) + (p4 & 1) * 4) * 2u;
+    }
+  }
+
+  float ma_run = -INFINITY, la = 0.f, mb_run = -INFINITY, lb = 0.f;
+  const float sl2 = a.scale * 1.4426950408889634f;
+  const int hb = 4 * h2;
+  auto mask_tile = [&](auto par) __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value;
+    advance(mc);
+    const int lim = mc.kend - mc.t0;
+    if (lim < KTT) {
+      if constexpr (P == 0) WB::mask_0(lim, hb); else WB::mask_1(lim, hb);
+    }
+  };
+  // attn_bf16_kernel's deferred running-max decision, per 32-query block
+  auto decide = [&](float& m_run, float& l_run, float mx, auto blk) __attribute__((always_inline)) {
+    mx = halves_max(mx);
+    if (__any(m_run == -INFINITY || (mx - m_run) * sl2 > 8.0f)) {
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha =
+          __builtin_amdgcn_exp2f(__builtin_fmaf(m_run, sl2, m_new == -INFINITY ? 0.f : -m_new * sl2));
+      l_run *= alpha;
+      if constexpr (decltype(blk)::value == 0) WB::rescale_0(alpha); else WB::rescale_1(alpha);
+      m_run = m_new;
+    }
+  };
+
+  WB::zero_o();
+  // prologue: K(0), V(0), K(1), K(2) after the Q loads; Q, K(0), V(0), K(1) waited (K(2) may stay in flight)
+  if (ntiles > 0) {
+    Dma d = next_dma(kc, 0);
+    WB::template dma_cs<0, 0>(r0, cx0, cx1, lw, d.last, d.ld2, d.base);
+    d = next_dma(vc, 1);
+    WB::template dma_cs<1, 0>(r0, cx0, cx1, lw, d.last, d.ld2, d.base);
+  }
+  if (ntiles > 1) {
+    const Dma d = next_dma(kc, 0);
+    WB::template dma_cs<0, 1>(r0, cx0, cx1, lw, d.last, d.ld2, d.base);
+  }
+  if (ntiles > 2) {
+    const Dma d = next_dma(kc, 0);
+    WB::template dma_cs<0, 2>(r0, cx0, cx1, lw, d.last, d.ld2, d.base);
+    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  if (ntiles > 0) {
+    WB::qk_0_0(ka);
+    mask_tile(std::integral_constant<int, 0>{});
+    float mxa, mxb;
+    WB::max_0(mxa, mxb);
+    decide(ma_run, la, mxa, std::integral_constant<int, 0>{});
+    decide(mb_run, lb, mxb, std::integral_constant<int, 1>{});
+  }
+  asm volatile("s_barrier" ::: "memory");  // every wave's K(0) reads are done: slot 0 takes K(3)
+
+  auto iter = [&](int t, auto unr) __attribute__((always_inline)) {
+    constexpr int U = decltype(unr)::value;  // t mod 6
+    constexpr int P = U & 1;                 // score buffer of tile t (its V slot too)
+    constexpr int KS = (U + 1) % 3;          // K slot of tile t + 1 (its QK runs in X(t))
+    constexpr int KD = U % 3;                // K slot that takes K(t + 3) (K(t) was read in X(t - 1))
+    const float msa = ma_run == -INFINITY ? 0.f : -ma_run * sl2;
+    const float msb = mb_run == -INFINITY ? 0.f : -mb_run * sl2;
+    float psa = 0.f, psb = 0.f;
+    if (t + 1 < ntiles) {
+      // X(t): V(t+1) -> V slot 1 - P (V(t-1) was read in Y(t-1))
+      const Dma dv = next_dma(vc, 1);
+      if constexpr ((ABL & 1) != 0) {
+        if constexpr (P == 0 && KS == 0) WB::xa_0_0(ka, sl2, msa, msb, psa, psb);
+        else if constexpr (P == 0 && KS == 1) WB::xa_0_1(ka, sl2, msa, msb, psa, psb);
+        else if constexpr (P == 0) WB::xa_0_2(ka, sl2, msa, msb, psa, psb);
+        else if constexpr (KS == 0) WB::xa_1_0(ka, sl2, msa, msb, psa, psb);
+        else if constexpr (KS == 1) WB::xa_1_1(ka, sl2, msa, msb, psa, psb);
+        else WB::xa_1_2(ka, sl2, msa, msb, psa, psb);
+        (void)dv;
+      } else {
+        if constexpr (P == 0 && KS == 0) WB::x_0_0(ka, sl2, msa, msb, psa, psb, r0, cx0, cx1, lw, dv.last, dv.ld2, dv.base);
+        else if constexpr (P == 0 && KS == 1) WB::x_0_1(ka, sl2, msa, msb, psa, psb, r0, cx0, cx1, lw, dv.last, dv.ld2, dv.base);
+        else if constexpr (P == 0) WB::x_0_2(ka, sl2, msa, msb, psa, psb, r0, cx0, cx1, lw, dv.last, dv.ld2, dv.base);
+        else if constexpr (KS == 0) WB::x_1_0(ka, sl2, msa, msb, psa, psb, r0, cx0, cx1, lw, dv.last, dv.ld2, dv.base);
+        else if constexpr (KS == 1) WB::x_1_1(ka, sl2, msa, msb, psa, psb, r0, cx0, cx1, lw, dv.last, dv.ld2, dv.base);
+        else WB::x_1_2(ka, sl2, msa, msb, psa, psb, r0, cx0, cx1, lw, dv.last, dv.ld2, dv.base);
+      }
+      mask_tile(std::integral_constant<int, 1 - P>{});
+      // Y(t): K(t+3) -> K slot KD, issued last in the iteration so that it may stay in flight across the barrier
+      float mxa, mxb;
+      const bool kdma = t + 3 < ntiles && !(ABL & 1);
+      if (kdma) {
+        const Dma dk = next_dma(kc, 0);
+        WB::template y_cs<P, KD>(va, sl2, msa, msb, psa, psb, mxa, mxb, r0, cx0, cx1, lw, dk.last, dk.ld2, dk.base);
+      } else {
+        WB::template y_cs<P, -1>(va, sl2, msa, msb, psa, psb, mxa, mxb, r0, cx0, cx1, lw, 0u, 0u, nullptr);
+      }
+      la += psa;
+      lb += psb;
+      decide(ma_run, la, mxa, std::integral_constant<int, 0>{});
+      decide(mb_run, lb, mxb, std::integral_constant<int, 1>{});
+      // V(t+1) and K(t+2) (issued before it) must have landed; K(t+3), issued last, may stay in flight
+      if constexpr ((ABL & 8) != 0) asm volatile("s_barrier" ::: "memory");
+      else if (kdma) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      if constexpr (P == 0) WB::xl_0(sl2, msa, msb, psa, psb); else WB::xl_1(sl2, msa, msb, psa, psb);
+      if constexpr (P == 0) WB::yl_0(va, sl2, msa, msb, psa, psb); else WB::yl_1(va, sl2, msa, msb, psa, psb);
+      la += psa;
+      lb += psb;
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  };
+  if (ABL & 16) ntiles = 0;
+  for (int t = 0; t < ntiles; t += 6) {
+    iter(t, std::integral_constant<int, 0>{});
+    if (t + 1 >= ntiles) break;
+    iter(t + 1, std::integral_constant<int, 1>{});
+    if (t + 2 >= ntiles) break;
+    iter(t + 2, std::integral_constant<int, 2>{});
+    if (t + 3 >= ntiles) break;
+    iter(t + 3, std::integral_constant<int, 3>{});
+    if (t + 4 >= ntiles) break;
+    iter(t + 4, std::integral_constant<int, 4>{});
+    if (t + 5 >= ntiles) break;
+    iter(t + 5, std::integral_constant<int, 5>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // (ablations / ntiles == 0: nothing may be in flight)
+
+  // ---- epilogue per q block (attn_pl_kernel's row layout): normalise, round, transpose through LDS, gate, store
+  auto store_block = [&](auto blk, float l_run) __attribute__((always_inline)) {
+    constexpr int J = decltype(blk)::value;
+    const float inv = 1.0f / halves_sum(l_run);
+    const int nv = a.n_q - (qw + 32 * J);  // wave-uniform
+    if (nv <= 0) return;
+    uint4 v4[8];
+    auto pack_dt = [&](const float (&od)[16], int dt) __attribute__((always_inline)) {
+      uint32_t wd[4][2];
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        wd[rg][0] = pack2bf(rbf(od[4 * rg + 0] * inv), rbf(od[4 * rg + 1] * inv));
+        wd[rg][1] = pack2bf(rbf(od[4 * rg + 2] * inv), rbf(od[4 * rg + 3] * inv));
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const auto x = __builtin_amdgcn_permlane32_swap(wd[2 * k][0], wd[2 * k + 1][0], false, false);
+        const auto y = __builtin_amdgcn_permlane32_swap(wd[2 * k][1], wd[2 * k + 1][1], false, false);
+        v4[2 * dt + k] = make_uint4(x[0], y[0], x[1], y[1]);
+      }
+    };
+    const int rl = lane >> 4, cc = lane & 15;
+    const int64_t qv = qw + 32 * J;
+    uint4 g4[8];
+    if (a.gate) {  // in flight during the pack and the transposition
+      const __amdgpu_buffer_rsrc_t gr =
+          attn_rsrc((const bf16_t*)a.gate + ECHO_QROW(a, row) * a.g_ld_batch + qv * a.g_ld_tok + head * 128,
+                    (uint32_t)(((int64_t)(min(nv, 32) - 1) * a.g_ld_tok + 128) * 2));
+      const uint32_t glo = (uint32_t)((rl * a.g_ld_tok + cc * 8) * 2), gst = (uint32_t)(a.g_ld_tok * 8);
+#pragma unroll
+      for (int pk = 0; pk < 8; ++pk) g4[pk] = attn_bload(gr, glo + pk * gst);
+    }
+    {
+      float od[16];
+      if constexpr (J == 0) {
+        WB::get_o_0_0(od); pack_dt(od, 0);
+        WB::get_o_0_1(od); pack_dt(od, 1);
+        WB::get_o_0_2(od); pack_dt(od, 2);
+        WB::get_o_0_3(od); pack_dt(od, 3);
+      } else {
+        WB::get_o_1_0(od); pack_dt(od, 0);
+        WB::get_o_1_1(od); pack_dt(od, 1);
+        WB::get_o_1_2(od); pack_dt(od, 2);
+        WB::get_o_1_3(od); pack_dt(od, 3);
+      }
+    }
+    bf16_t* sw = lds + (2 * w + J) * 32 * 128;  // free: no DMA in flight, every wave passed the last barrier
+#pragma unroll
+    for (int pk = 0; pk < 8; ++pk) *(uint4*)(sw + ql * 128 + (((2 * pk + h2) ^ (ql & 15)) * 8)) = v4[pk];
+#pragma unroll
+    for (int pk = 0; pk < 8; ++pk) {
+      const int r = pk * 4 + rl;
+      v4[pk] = *(const uint4*)(sw + r * 128 + ((cc ^ (r & 15)) * 8));
+    }
+    if (a.gate) attn_gate(v4, g4);
+    attn_store_rows(v4, (bf16_t*)a.out + row * a.o_ld_batch + qv * a.o_ld_tok + head * 128, nv, a.o_ld_tok, lane);
+  };
+  store_block(std::integral_constant<int, 0>{}, la);
+  store_block(std::integral_constant<int, 1>{}, lb);
+}
 #pragma clang diagnostic pop
 
 // one (query qi, 8 output columns c8) unit of (row, head) rh of the split-KV combine
@@ -1183,6 +1446,23 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 16: hipLaunchKernelGGL(attn_pl_kernel<16>, grid, dim3(256), 0, s, *a); break;
     case 17: hipLaunchKernelGGL(attn_pl_kernel<6>, grid, dim3(256), 0, s, *a); break;
     case 18: hipLaunchKernelGGL(attn_pl_kernel<7>, grid, dim3(256), 0, s, *a); break;
+    case 30: case 31: case 32: case 33:  // one wave per SIMD, 64 queries per wave (31-33: ablations 16 no tile
+      // loop, 1 no loop DMA, 8 no end-of-tile wait)
+      if (any_causal(a)) return ECHO_EINVAL;
+      if (cfg == 30) hipLaunchKernelGGL((attn_w64_kernel<0, 2>), grid, dim3(128), 0, s, *a);
+      else if (cfg == 31) hipLaunchKernelGGL((attn_w64_kernel<16, 2>), grid, dim3(128), 0, s, *a);
+      else if (cfg == 32) hipLaunchKernelGGL((attn_w64_kernel<1, 2>), grid, dim3(128), 0, s, *a);
+      else hipLaunchKernelGGL((attn_w64_kernel<8, 2>), grid, dim3(128), 0, s, *a);
+      break;
+    case 40: case 41: case 42: case 43: {  // 4 waves x 64 queries (256-query workgroups; 41-43: ablations as 31-33)
+      if (any_causal(a)) return ECHO_EINVAL;
+      const dim3 g4(attn_grid(a, 256));
+      if (cfg == 40) hipLaunchKernelGGL((attn_w64_kernel<0, 4>), g4, dim3(256), 0, s, *a);
+      else if (cfg == 41) hipLaunchKernelGGL((attn_w64_kernel<16, 4>), g4, dim3(256), 0, s, *a);
+      else if (cfg == 42) hipLaunchKernelGGL((attn_w64_kernel<1, 4>), g4, dim3(256), 0, s, *a);
+      else hipLaunchKernelGGL((attn_w64_kernel<8, 4>), g4, dim3(256), 0, s, *a);
+      break;
+    }
     case 20: case 21: case 22: {  // asm pipeline at 8 waves x 32 queries (21: no tile loop, 22: no X / Y bodies)
       if (any_causal(a)) return ECHO_EINVAL;
       const dim3 g8(attn_grid(a, 256));
@@ -1215,7 +1495,9 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
     // each wave issues twice the DMA; that case takes split-KV chains, echo_attention_split)
     // non-causal launches (every decoder attention) run the asm-owned pipeline (attn_pl_kernel, bitwise
     // equal to attn_bf16_kernel<0, 4, 2>); causal ones (speaker / latent encoders) the compiler-scheduled kernel
-    if (g_attn_pl && !any_causal(a))
+    if (g_attn_pl == 2 && !any_causal(a))
+      hipLaunchKernelGGL((attn_w64_kernel<0, 4>), dim3(attn_grid(a, 256)), dim3(256), 0, s, *a);
+    else if (g_attn_pl && !any_causal(a))
       hipLaunchKernelGGL(attn_pl_kernel<0>, dim3(attn_grid(a, 128)), dim3(256), 0, s, *a);
     else
       hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1);
@@ -1272,7 +1554,7 @@ extern "C" int32_t echo_attention_pick_split(const EchoAttnArgs* a) {
 }
 
 extern "C" int echo_attention_set_pipeline(int32_t on) {
-  if (on < 0 || on > 1) return ECHO_EINVAL;
+  if (on < 0 || on > 2) return ECHO_EINVAL;
   g_attn_pl = on;
   return 0;
 }

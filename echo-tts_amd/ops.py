@@ -186,10 +186,11 @@ def gemm_no_splitk():
     return _knob("gemm_no_splitk", 1)
 
 
-def attention_pipeline(on: bool):
-    """Route non-causal bf16 attention launches to the asm-owned pipelined kernel (True, the default)
-    or to the compiler-scheduled kernel (False) inside the block (A/B tests and measurements)."""
-    return _knob("attention_pipeline", int(bool(on)))
+def attention_pipeline(mode):
+    """The kernel of non-causal bf16 attention launches inside the block (A/B tests and measurements):
+    1 / True = the asm-owned pipelined kernel (attn_pl_kernel, default), 0 / False = the compiler-scheduled
+    kernel, 2 = one wave per SIMD with 64 queries per wave (attn_w64_kernel). All bitwise equal."""
+    return _knob("attention_pipeline", int(mode))
 
 
 @contextlib.contextmanager

@@ -542,6 +542,17 @@ def test_attention_pipeline_bitwise(case):
         got.fill_(float("nan"))
         ops.attention(q[:, :, 0], segs, out=got, gate=gate)
     assert torch.equal(got, ref)
+    # one wave per SIMD, 64 queries per wave (attn_w64_kernel, 2 / 4 waves per workgroup): the variant entry and
+    # the production op
+    for v in (30, 40):
+        got.fill_(float("nan"))
+        ops.attention_variant(q[:, :, 0], segs, out=got, gate=gate, variant=v)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref), (v, float((got != ref).double().mean()))
+    with ops.attention_pipeline(2), ops.attention_split(1):
+        got.fill_(float("nan"))
+        ops.attention(q[:, :, 0], segs, out=got, gate=gate)
+    assert torch.equal(got, ref)
     if case in ("one_tile", "one_query", "spikes"):
         close_bf16(ref, ref_attention(q[:, :, 0], segs, gate, 128 ** -0.5, BF))
 
