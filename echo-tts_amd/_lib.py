@@ -70,6 +70,7 @@ SIGNATURES = {
     "echo_gemm_pick_tile": (i32, [i32, i32, i32, i32]),
     "echo_gemm_set_diag": (i32, [i32, i32]),
     "echo_gemm_ws_bytes": (i64, [C.POINTER(GemmArgs)]),
+    "echo_gemm_planned_tile": (i32, [C.POINTER(GemmArgs), i64]),
     "echo_gemm_ws": (i32, [C.POINTER(GemmArgs), vp, i64, vp]),
     "echo_set_policy_rows": (i32, [i32, i32]),
     "echo_attention": (i32, [C.POINTER(AttnArgs), vp]),

@@ -429,7 +429,7 @@ int echo_cast_from_f32(int32_t dtype, const float* x, void* y, int64_t n, void* 
   return 0;
 }
 
-const char* echo_version(void) { return "echo_hip gfx950 r4 abi5 " __DATE__ " " __TIME__; }
+const char* echo_version(void) { return "echo_hip gfx950 r5 abi6 " __DATE__ " " __TIME__; }
 
 int32_t echo_abi_version(void) { return ECHO_ABI_VERSION; }
 

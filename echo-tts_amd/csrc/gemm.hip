@@ -2658,6 +2658,21 @@ extern "C" int64_t echo_gemm_ws_bytes(const EchoGemmArgs* a) {
   return 0;
 }
 
+// the launch echo_gemm_ws would make for these arguments with a workspace of ws_bytes (host only; perf_model.py
+// labels its timed launches with it): 100 + 10 c + S for the small-M config c split S ways, else the large-tile
+// pick (13 = the 256x256 / 320x256 family)
+extern "C" int32_t echo_gemm_planned_tile(const EchoGemmArgs* a, int64_t ws_bytes) {
+  if (!a || a->M <= 0 || a->N <= 0 || a->K <= 0 || a->K % BK) return 0;
+  if (a->tile != 0) return a->tile;
+  int c = 0, S = 1;
+  if (sk_plan(a, ws_bytes > 0, &c, &S)) {
+    const int64_t need = sk_ws_bytes(a, c, S);
+    if (need == 0 || ws_bytes >= need) return 100 + 10 * c + S;
+    if (sk_plan(a, false, &c, &S) && sk_ws_bytes(a, c, S) == 0) return 100 + 10 * c + S;
+  }
+  return echo_gemm_pick_tile(a->M, a->N, a->K, a->batch);
+}
+
 extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) { return echo_gemm_ws(a, nullptr, 0, stream); }
 
 extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, void* stream) {

@@ -75,9 +75,30 @@ def blockwise_flops(cfg: EchoConfig, block_sizes: Sequence[int], steps_cfg: int,
     return out
 
 
+def planned_tile(a, w, out, epilogue: int, aux=None) -> int:
+    """The launch the library plans for this GEMM (echo_gemm_planned_tile with the workspace the torch op would
+    allocate): 100 + 10 c + S for the small-M config c split S ways, else the large-tile pick."""
+    from . import _lib
+    lib = _lib.load()
+    g = _lib.GemmArgs()
+    g.dtype = 0 if a.dtype == torch.bfloat16 else 1
+    g.M, g.K, g.N, g.batch = a.shape[-2], a.shape[-1], w.shape[-2], 1
+    g.A, g.W = a.data_ptr(), w.data_ptr()
+    g.C = out.data_ptr() if out is not None else a.data_ptr()
+    g.lda, g.ldw = a.stride(-2), w.stride(-2)
+    g.ldc = out.stride(-2) if out is not None else g.N
+    g.epilogue = epilogue
+    if aux is not None:
+        g.aux, g.ld_aux = aux.data_ptr(), aux.stride(-2)
+    import ctypes
+    return int(lib.echo_gemm_planned_tile(ctypes.byref(g), lib.echo_gemm_ws_bytes(ctypes.byref(g))))
+
+
 class GemmTimer:
     """Wraps ops.gemm: HIP events around every launch of one tile config on the launch
-    stream, plus its algorithmic FLOPs (2·M·N·K·batch) — for roofline.achieved."""
+    stream, plus its algorithmic FLOPs (2·M·N·K·batch) — for roofline.achieved. With tile_filter None (the B = 1
+    legs: every GEMM launch) the fused residual + next AdaLN (ops.gemm_resid_norm) is timed as the one call
+    production makes, and every record carries the launch the library planned (planned_tile)."""
 
     def __init__(self, tile_filter=None):
         self.records: List = []
@@ -107,15 +128,29 @@ class GemmTimer:
             osz = 4 if kw.get("epilogue", 0) == _lib.EPI_F32OUT else 2
             byts = 2 * (M * K * (a.shape[0] if a.dim() == 3 else 1) + N * K * (w.shape[0] if w.dim() == 3 else 1)) \
                 + osz * M * nout * batch + (2 * M * nout * batch if kw.get("aux") is not None else 0)
-            timer.records.append((e0, e1, 2.0 * M * N * K * batch, tile, (M, N, K, batch), byts))
+            lab = planned_tile(a, w, out, kw.get("epilogue", 0), kw.get("aux")) if batch == 1 and a.dim() == 2 else tile
+            timer.records.append((e0, e1, 2.0 * M * N * K * batch, lab, (M, N, K, batch), byts))
             return r
 
         def wrapped_rn(a, w, h, gate, shift, scale1, eps, xn, tile=0):
-            # the gated residual + next AdaLN (ops.gemm_resid_norm) as its two parts, the GEMM timed like any
-            # other: bitwise the fused call (at the large-tile shapes it IS these two kernels)
-            wrapped(a, w, out=h, epilogue=_lib.EPI_RESID, aux=h, gate=gate, tile=tile)
-            ops.adaln_modulate(h, shift, scale1, eps, xn)
-            return xn
+            if timer.tile_filter is not None:
+                # the large-tile family: the gated residual + next AdaLN as its two parts, the GEMM timed like any
+                # other (bitwise the fused call; at the large-tile shapes it IS these two kernels)
+                wrapped(a, w, out=h, epilogue=_lib.EPI_RESID, aux=h, gate=gate, tile=tile)
+                ops.adaln_modulate(h, shift, scale1, eps, xn)
+                return xn
+            # every launch (B = 1 legs): the one fused call production makes (split-K finish with the AdaLN fused
+            # where the small-M plan has a finish kernel), events around all of it; bytes include xn's write
+            M, K, N = a.shape[-2], a.shape[-1], w.shape[-2]
+            s = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            r = timer._orig_rn(a, w, h, gate, shift, scale1, eps, xn, tile)
+            e1.record(s)
+            byts = 2 * (M * K + N * K) + 2 * M * N * 3
+            timer.records.append((e0, e1, 2.0 * M * N * K, planned_tile(a, w, h, _lib.EPI_RESID, h),
+                                  (M, N, K, 1), byts))
+            return r
 
         self._orig_rn = ops.gemm_resid_norm
         ops.gemm = wrapped
@@ -137,9 +172,12 @@ class GemmTimer:
         avg_ms = sum(ms) / n
         avg_fl = sum(fl) / n
         avg_b = sum(r[5] for r in self.records) / n
+        tiles: Dict[str, int] = {}
+        for r in self.records:
+            tiles[str(r[3])] = tiles.get(str(r[3]), 0) + 1
         return {"launches": n, "avg_ms": avg_ms, "avg_flop": avg_fl, "avg_bytes": avg_b,
                 "tflops": avg_fl / (avg_ms * 1e-3) / 1e12, "gbs": avg_b / (avg_ms * 1e-3) / 1e9,
-                "total_ms": avg_ms * n}
+                "total_ms": avg_ms * n, "planned_tiles": tiles}
 
 
 class AttnTimer:

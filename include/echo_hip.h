@@ -102,6 +102,9 @@ int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch);
  * split launch sums K in S contiguous partial sums (fp32; the unsplit kernels all share one K order).
  * The workspace is only touched by the launched kernels (stream-ordered, capturable). */
 int64_t echo_gemm_ws_bytes(const EchoGemmArgs* args);
+/* Host-only query: the launch echo_gemm_ws(args, ws, ws_bytes, .) would make — 100 + 10 c + S for the small-M
+ * config c with K split S ways, otherwise echo_gemm_pick_tile's large-tile pick (bench.py's per-launch labels). */
+int32_t echo_gemm_planned_tile(const EchoGemmArgs* args, int64_t ws_bytes);
 int echo_gemm_ws(const EchoGemmArgs* args, void* ws, int64_t ws_bytes, void* stream);
 
 /* Split decisions (GEMM split-K here, split-KV in echo_attention_pick_split) depend on the launch's

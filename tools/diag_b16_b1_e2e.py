@@ -117,3 +117,44 @@ def garbage_test():
 
 if __name__ == "__main__" and os.environ.get("DIAG_GARBAGE"):
     garbage_test()
+
+
+def scratch_test():
+    """Does setup() (text / speaker encoders + KV projections) read memory it never wrote? Pre-fill the caching
+    allocator's blocks (a large tensor, freed) with NaN / 0 / random before each setup of the SAME plan."""
+    S = W.synthetic_state_dict(E.FULL, dtype=torch.bfloat16, include_latent=False)
+    m = EchoDiTHip(E.FULL, S, device=DEV, dtype=torch.bfloat16)
+    del S
+    ids, tm = SY.text_inputs(1)
+    spk, sm = SY.speaker_inputs(1)
+    noise = torch.randn((1, 640, 80), generator=torch.Generator().manual_seed(77))
+    ids, tm, spk, sm, noise = (t.to(DEV) for t in (ids, tm, spk, sm, noise))
+    sched = En.make_schedule(40, 3.0, 8.0, 0.5, 1.0, None, None, None, None, device=DEV)
+    Tc, Pc = En.caps(m, ids, tm, spk, sm)
+    p = En.CFGPlan(m, 1, 640, Tc, Pc, sched, None, None)
+    res = {}
+    for fill in ("zero", "nan", "rand", "zero"):
+        big = torch.empty((6 << 30) // 2, device=DEV, dtype=torch.bfloat16)
+        if fill == "nan":
+            big.fill_(float("nan"))
+        elif fill == "zero":
+            big.zero_()
+        else:
+            big.normal_()
+        del big
+        with ops.attention_split(1), ops.gemm_no_splitk():
+            p.setup(ids, tm, spk, sm, noise, None)
+        torch.cuda.synchronize()
+        ks, kt = p.kv_spk.clone(), p.kv_text.clone()
+        print(f"fill {fill}: kv_spk finite {bool(torch.isfinite(ks.float()).all())} kv_text finite "
+              f"{bool(torch.isfinite(kt.float()).all())}", flush=True)
+        res.setdefault(fill, []).append((ks, kt))
+    base = res["zero"][0]
+    for k, v in res.items():
+        for ks, kt in v:
+            print(f"fill {k}: kv_spk == zero-fill run {torch.equal(ks, base[0])}, kv_text {torch.equal(kt, base[1])}",
+                  flush=True)
+
+
+if __name__ == "__main__" and os.environ.get("DIAG_SCRATCH"):
+    scratch_test()
