@@ -1175,7 +1175,10 @@ gemm_bf16_ps_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
   if constexpr (EK == EK_BIAS) load_bias(n0, bb);
   prologue();
 
-  const __amdgpu_buffer_rsrc_t crs = brsrc((bf16_t*)Cv + z * sC, (uint32_t)(((int64_t)(M - 1) * ldc + N) * 2));
+  // the output's last row ends at column N (N / 2 for SwiGLU, whose output holds half the GEMM's columns): with
+  // N there, row M would lie inside num_records whenever ldc < N, and the last tile row past M would be stored
+  const __amdgpu_buffer_rsrc_t crs =
+      brsrc((bf16_t*)Cv + z * sC, (uint32_t)(((int64_t)(M - 1) * ldc + (EK == EK_SWIGLU ? N / 2 : N)) * 2));
   const int frow = lane & 15;
   const int fsw = frow >> 1;
   bool first = true;

@@ -962,6 +962,41 @@ def test_gemm_split_k_epilogues_vs_fp64(M, N, K, epi):
         print(f"[split-K epi {epi} M={M} N={N} K={K} tile {tile}] <=1 ulp {frac:.5f}  max {int(d.max())} ulp")
         assert frac >= 0.999, (tile, frac)
 
+
+@pytest.mark.parametrize("epi", [L.EPI_STORE, L.EPI_SWIGLU, L.EPI_RESID])
+def test_gemm_no_store_past_m(epi):
+    """No GEMM launch writes past its M rows: out is the first M rows of a buffer whose guard rows hold a
+    sentinel, for every large-tile config, the auto pick (row split, 320-row tiles) and small-M split-K
+    plans, at M with a partial last tile row. (The 2-phase 256x256 kernel's SwiGLU store bound once used the
+    GEMM's N for the output's N / 2 columns and wrote row M, which at B = 1 landed in the speaker KV cache
+    allocated right after the W13 output.)"""
+    K = 512
+    torch.manual_seed(epi)
+    for M, N in ((1920, 2048), (1000, 1024), (333, 512), (160, 2048)):
+        nout = N // 2 if epi == L.EPI_SWIGLU else N
+        a = torch.randn(M, K, device=DEV).to(BF)
+        w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+        g = (torch.rand(N, device=DEV) + 0.5).to(BF)
+        h0 = torch.randn(M, nout, device=DEV).to(BF)
+        ran = 0
+        for tile in (0, 1, 2, 3, 4, 5, 13, 16, 112, 131, 164):
+            buf = torch.full((M + 4, nout), 7.0, device=DEV, dtype=BF)
+            out = buf[:M]
+            try:
+                if epi == L.EPI_RESID:
+                    out.copy_(h0)
+                    ops.gemm(a, w, out=out, epilogue=epi, aux=out, gate=g, tile=tile)
+                else:
+                    ops.gemm(a, w, out=out, epilogue=epi, tile=tile)
+            except RuntimeError:  # config rejects the shape
+                continue
+            torch.cuda.synchronize()
+            ran += 1
+            assert bool((buf[M:] == 7.0).all()), (M, N, tile, int((buf[M:] != 7.0).sum()))
+        assert ran >= 3, (M, N, ran)
+
+
+def test_gemm_small_m_policy_rows():
     """echo_set_policy_rows: the split decision for a launch of M rows taken as for M * num / den rows —
     a rank holding 1 of 8 prompts splits K exactly like the one-process run of 8 prompts (here: not at
     all), so its rows are bitwise those of that run."""
