@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU-box helper (round 5): one UNFILTERED rocprofv3 FETCH_SIZE pass over `bench.py --workload c2 --no-graph`
+# GPU-box helper: one UNFILTERED rocprofv3 FETCH_SIZE pass over `bench.py --workload c2 --no-graph`
 # (the pass that crashed once in round 4), with the process's memory map written after the warm-up call so
 # that a native crash trace can be symbolized (tools/symbolize_frames.py).
 set -o pipefail
