@@ -4,7 +4,11 @@
 
 Objects go to `echo-tts_amd/build/`, the library to `echo-tts_amd/libecho_hip.so`
 (git-ignored; it travels to the GPU box with the snapshot). Rebuilds only when a
-source or header is newer than the library.
+source or header is newer than the library, or the flags changed.
+
+ECHO_DIAG=1 builds the diagnostics library instead: it adds the timing ablations of the attention kernels
+(`echo_attention_variant` ablation bits and variants 12-22 / 31-43), which the product library
+leaves out. Build the product library again (without ECHO_DIAG) before tests, smoke or bench.
 """
 from __future__ import annotations
 
@@ -22,7 +26,8 @@ OBJ = os.path.join(PKG, "build")
 SOURCES = ["gemm.hip", "attention.hip", "elementwise.hip", "codec.hip"]
 HEADERS = [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "attn_pl.inc"), os.path.join(CSRC, "attn_w64.inc"), os.path.join(REPO, "include", "echo_hip.h")]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
-         "-Wno-unused-result"]
+         "-Wno-unused-result"] + (["-DECHO_DIAG"] if os.environ.get("ECHO_DIAG") == "1" else [])
+STAMP = os.path.join(OBJ, "flags.txt")  # the flags the objects were built with
 
 
 def _hipcc() -> str:
@@ -66,6 +71,9 @@ def build_torch_ops(force: bool = False, verbose: bool = True) -> str:
 def build(force: bool = False, verbose: bool = True) -> str:
     os.makedirs(OBJ, exist_ok=True)
     hipcc = _hipcc()
+    flags = " ".join(FLAGS)
+    if not os.path.exists(STAMP) or open(STAMP).read() != flags:
+        force = True
     jobs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
@@ -92,8 +100,10 @@ def build(force: bool = False, verbose: bool = True) -> str:
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
         os.replace(tmp, OUT)
+        with open(STAMP, "w") as f:
+            f.write(flags)
         if verbose:
-            print(f"built {OUT}")
+            print(f"built {OUT}" + (" (diagnostics build)" if "-DECHO_DIAG" in FLAGS else ""))
     build_torch_ops(force, verbose)
     return OUT
 

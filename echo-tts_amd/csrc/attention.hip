@@ -1200,297 +1200,6 @@ __global__ void __launch_bounds__(64 * NW, 1) __attribute__((amdgpu_num_vgpr(128
   store_block(std::integral_constant<int, 1>{}, lb);
 }
 
-// attn_w64p_kernel: the persistent form of attn_w64_kernel<., 4> (one 256-query workgroup per CU walks the items
-// blockIdx.x + k gridDim.x). Item i+1's Q rows (into the Q registers, free after item i's last QK) and its first
-// three K tiles are loaded under item i's last tile, its first V tile under item i's epilogue, so the item seam
-// costs one drain of those loads and of item i's output stores instead of a cold prologue. The epilogue stores
-// each lane's rows straight from the accumulator layout (attn_pack_out / attn_write_out: the K / V ring is being
-// refilled, so no LDS transposition). Same tile math per 32-query block: bitwise equal to attn_w64_kernel.
-// Per-item segment tables are re-read from the kernel arguments by each cursor when it crosses a segment.
-template <int ABL>
-__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_num_vgpr(128))) attn_w64p_kernel(EchoAttnArgs a_arg) {
-  using WB = W4;
-  constexpr int NW = 4, QB = 256, KTT = KT;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[5 * KT * 128];  // K slots 0-2 | V slots 0-1 (80 KiB)
-  using KArgs = const __attribute__((address_space(4))) EchoAttnArgs;
-  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  (void)a_arg;
-  const int nqb = (a.n_q + QB - 1) / QB;
-  const int nitems = nqb * a.rows * a.heads;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h2 = lane >> 5, ql = lane & 31;
-
-  // per-item cursor over the flat tile list [self | latent | text | speaker] of (row, head); non-causal
-  struct PCur {  // part: 0 = K, 1 = V (the base pointer it tracks)
-    int row, head, seg, t0, left, kend, ld;
-    const bf16_t* base;
-  };
-  auto seg_end = [&](int sg, int row) __attribute__((always_inline)) {
-    if (sg >= a.nseg || !a.seg[sg].k) return 0;
-    const int len = a.seg[sg].len ? a.seg[sg].len[row] : a.seg[sg].capacity;
-    return max(min(len, a.seg[sg].capacity), 0);
-  };
-  auto begin = [&](PCur& c, int row, int head) __attribute__((always_inline)) {
-    c.row = row; c.head = head; c.seg = -1; c.left = 0; c.t0 = 0; c.kend = 0; c.ld = 0; c.base = nullptr;
-  };
-  auto advance = [&](PCur& c, int part) __attribute__((always_inline)) {
-    if (c.left == 0) {
-      int ke = 0;
-      do { ++c.seg; ke = seg_end(c.seg, c.row); } while (c.seg < 3 && ke <= 0);
-      if (part >= 0) {
-        const int b_ = c.row % a.seg[c.seg].batch_mod;
-        c.base = (const bf16_t*)(part ? a.seg[c.seg].v : a.seg[c.seg].k) + b_ * a.seg[c.seg].ld_batch + c.head * 128;
-        c.ld = (int)a.seg[c.seg].ld_tok;
-      }
-      c.kend = ke;
-      c.t0 = 0;
-      c.left = (ke + KTT - 1) / KTT;
-    } else {
-      c.t0 += KTT;
-    }
-    --c.left;
-  };
-  auto item_tiles = [&](int row) __attribute__((always_inline)) {
-    int n = 0;
-#pragma unroll
-    for (int sg = 0; sg < 4; ++sg) n += (seg_end(sg, row) + KTT - 1) / KTT;
-    return n;
-  };
-  struct Item {
-    int row, head, qw, ntiles;
-  };
-  auto item_of = [&](int L) __attribute__((always_inline)) {
-    Item it;
-    const int Lr = L / nqb;  // rows fastest
-    it.row = Lr % a.rows;
-    it.head = Lr / a.rows;
-    it.qw = (L % nqb) * QB + 64 * w;
-    it.ntiles = item_tiles(it.row);
-    return it;
-  };
-
-  const int dr = lane >> 4, dp = lane & 15;
-  const uint32_t r0 = (uint32_t)(4 * w + dr);
-  const uint32_t cx0 = (uint32_t)((dp ^ ((dr << 2) | w)) * 16);
-  const uint32_t lbase = lds_addr_of(lds);
-  const uint32_t lw = __builtin_amdgcn_readfirstlane(lbase + (uint32_t)w * 1024u);
-  struct Dma {
-    const void* base;
-    uint32_t last, ld2;
-  };
-  auto next_dma = [&](PCur& c, int part) __attribute__((always_inline)) {
-    advance(c, part);
-    // wave-uniform by construction; readfirstlane lets the asm's "s" operands take them when hipcc cannot prove it
-    const uint64_t pb = (uint64_t)(uintptr_t)(c.base + (int64_t)c.t0 * c.ld);
-    Dma d;
-    d.base = (const void*)uniform_u64(pb);
-    d.last = __builtin_amdgcn_readfirstlane((uint32_t)(c.kend - 1 - c.t0));
-    d.ld2 = __builtin_amdgcn_readfirstlane((uint32_t)c.ld * 2u);
-    return d;
-  };
-  auto load_q = [&](const Item& it) __attribute__((always_inline)) {
-    const int qca = min(it.qw + ql, a.n_q - 1), qcb = min(it.qw + 32 + ql, a.n_q - 1);
-    const bf16_t* qbase = (const bf16_t*)a.q + ECHO_QROW(a, it.row) * a.q_ld_batch + it.head * 128;
-    WB::load_q((uint32_t)(((int64_t)qca * a.q_ld_tok + 8 * h2) * 2), (uint32_t)(((int64_t)qcb * a.q_ld_tok + 8 * h2) * 2),
-               qbase);
-  };
-
-  uint32_t ka[8], va[8];
-#pragma unroll
-  for (int ds = 0; ds < 8; ++ds) ka[ds] = lbase + (uint32_t)(ql * 128 + (((2 * ds + h2) ^ swz(ql)) * 8)) * 2u;
-  {
-    const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-    const int rr0 = 4 * h2 + q4, rr1 = rr0 + 8;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int ch = 4 * dt + 2 * (g & 1) + (p4 >> 1);
-      va[2 * dt] = lbase + 3u * KT * 128 * 2 + (uint32_t)(rr0 * 128 + ((ch ^ swz(rr0)) * 8) + (p4 & 1) * 4) * 2u;
-      va[2 * dt + 1] = lbase + 3u * KT * 128 * 2 + (uint32_t)(rr1 * 128 + ((ch ^ swz(rr1)) * 8) + (p4 & 1) * 4) * 2u;
-    }
-  }
-  const float sl2 = a.scale * 1.4426950408889634f;
-  const int hb = 4 * h2;
-  float ma_run, la, mb_run, lb;
-  auto decide = [&](float& m_run, float& l_run, float mx, auto blk) __attribute__((always_inline)) {
-    mx = halves_max(mx);
-    if (__any(m_run == -INFINITY || (mx - m_run) * sl2 > 8.0f)) {
-      const float m_new = fmaxf(m_run, mx);
-      const float alpha =
-          __builtin_amdgcn_exp2f(__builtin_fmaf(m_run, sl2, m_new == -INFINITY ? 0.f : -m_new * sl2));
-      l_run *= alpha;
-      if constexpr (decltype(blk)::value == 0) WB::rescale_0(alpha); else WB::rescale_1(alpha);
-      m_run = m_new;
-    }
-  };
-
-  int L = blockIdx.x;
-  if (L >= nitems) return;
-  Item cur = item_of(L);
-  PCur kc, vc, mc;
-  begin(kc, cur.row, cur.head);
-  begin(vc, cur.row, cur.head);
-  // cold prologue of the first item: Q, K(0..2), V(0)
-  load_q(cur);
-  {
-    int nt = cur.ntiles;
-    if (nt > 0) { Dma d = next_dma(kc, 0); WB::template dma_cs<0, 0>(r0, cx0, cx0, lw, d.last, d.ld2, d.base); }
-    if (nt > 1) { Dma d = next_dma(kc, 0); WB::template dma_cs<0, 1>(r0, cx0, cx0, lw, d.last, d.ld2, d.base); }
-    if (nt > 2) { Dma d = next_dma(kc, 0); WB::template dma_cs<0, 2>(r0, cx0, cx0, lw, d.last, d.ld2, d.base); }
-    if (nt > 0) { Dma d = next_dma(vc, 1); WB::template dma_cs<1, 0>(r0, cx0, cx0, lw, d.last, d.ld2, d.base); }
-  }
-  WB::zero_o();
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  while (true) {
-    const int ntiles = cur.ntiles;
-    begin(mc, cur.row, cur.head);
-    ma_run = -INFINITY; la = 0.f; mb_run = -INFINITY; lb = 0.f;
-    auto mask_tile = [&](auto par) __attribute__((always_inline)) {
-      constexpr int P = decltype(par)::value;
-      advance(mc, -1);
-      const int lim = mc.kend - mc.t0;
-      if (lim < KTT) {
-        if constexpr (P == 0) WB::mask_0(lim, hb); else WB::mask_1(lim, hb);
-      }
-    };
-    if (ntiles > 0) {
-      WB::qk_0_0(ka);
-      mask_tile(std::integral_constant<int, 0>{});
-      float mxa, mxb;
-      WB::max_0(mxa, mxb);
-      decide(ma_run, la, mxa, std::integral_constant<int, 0>{});
-      decide(mb_run, lb, mxb, std::integral_constant<int, 1>{});
-    }
-    asm volatile("s_barrier" ::: "memory");  // every wave's K(0) reads are done: slot 0 takes K(3)
-    const int nxt = L + (int)gridDim.x;
-    const bool has_next = nxt < nitems;
-    Item nit;
-    auto iter = [&](int t, auto unr) __attribute__((always_inline)) {
-      constexpr int U = decltype(unr)::value;  // t mod 6
-      constexpr int P = U & 1;
-      constexpr int KS = (U + 1) % 3;
-      constexpr int KD = U % 3;
-      const float msa = ma_run == -INFINITY ? 0.f : -ma_run * sl2;
-      const float msb = mb_run == -INFINITY ? 0.f : -mb_run * sl2;
-      float psa = 0.f, psb = 0.f;
-      if (t + 1 < ntiles) {
-        const Dma dv = next_dma(vc, 1);
-        if constexpr (P == 0 && KS == 0) WB::x_0_0(ka, sl2, msa, msb, psa, psb, r0, cx0, cx0, lw, dv.last, dv.ld2, dv.base);
-        else if constexpr (P == 0 && KS == 1) WB::x_0_1(ka, sl2, msa, msb, psa, psb, r0, cx0, cx0, lw, dv.last, dv.ld2, dv.base);
-        else if constexpr (P == 0) WB::x_0_2(ka, sl2, msa, msb, psa, psb, r0, cx0, cx0, lw, dv.last, dv.ld2, dv.base);
-        else if constexpr (KS == 0) WB::x_1_0(ka, sl2, msa, msb, psa, psb, r0, cx0, cx0, lw, dv.last, dv.ld2, dv.base);
-        else if constexpr (KS == 1) WB::x_1_1(ka, sl2, msa, msb, psa, psb, r0, cx0, cx0, lw, dv.last, dv.ld2, dv.base);
-        else WB::x_1_2(ka, sl2, msa, msb, psa, psb, r0, cx0, cx0, lw, dv.last, dv.ld2, dv.base);
-        mask_tile(std::integral_constant<int, 1 - P>{});
-        float mxa, mxb;
-        const bool kdma = t + 3 < ntiles;
-        if (kdma) {
-          const Dma dk = next_dma(kc, 0);
-          WB::template y_cs<P, KD>(va, sl2, msa, msb, psa, psb, mxa, mxb, r0, cx0, cx0, lw, dk.last, dk.ld2, dk.base);
-        } else {
-          WB::template y_cs<P, -1>(va, sl2, msa, msb, psa, psb, mxa, mxb, r0, cx0, cx0, lw, 0u, 0u, nullptr);
-        }
-        la += psa;
-        lb += psb;
-        decide(ma_run, la, mxa, std::integral_constant<int, 0>{});
-        decide(mb_run, lb, mxb, std::integral_constant<int, 1>{});
-        if (kdma) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");  // K(t+3): 4 pieces per wave
-        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      } else {
-        // the last tile: the next item's Q (its registers are free after this item's last QK) and first three K
-        // tiles (every K slot is free) go out first, under this tile's softmax and PV
-        if (has_next) {
-          nit = item_of(nxt);
-          load_q(nit);
-          begin(kc, nit.row, nit.head);
-          const int nt = nit.ntiles;
-          if (nt > 0) { Dma d = next_dma(kc, 0); WB::template dma_cs<0, 0>(r0, cx0, cx0, lw, d.last, d.ld2, d.base); }
-          if (nt > 1) { Dma d = next_dma(kc, 0); WB::template dma_cs<0, 1>(r0, cx0, cx0, lw, d.last, d.ld2, d.base); }
-          if (nt > 2) { Dma d = next_dma(kc, 0); WB::template dma_cs<0, 2>(r0, cx0, cx0, lw, d.last, d.ld2, d.base); }
-        }
-        if constexpr (P == 0) WB::xl_0(sl2, msa, msb, psa, psb); else WB::xl_1(sl2, msa, msb, psa, psb);
-        if constexpr (P == 0) WB::yl_0(va, sl2, msa, msb, psa, psb); else WB::yl_1(va, sl2, msa, msb, psa, psb);
-        la += psa;
-        lb += psb;
-        asm volatile("s_barrier" ::: "memory");  // every wave's V reads are done: V slot 0 takes the next V(0)
-      }
-    };
-    if (ABL & 16) {
-      if (has_next) {
-        nit = item_of(nxt);
-        load_q(nit);
-        begin(kc, nit.row, nit.head);
-      }
-    } else {
-      for (int t = 0; t < ntiles; t += 6) {
-        iter(t, std::integral_constant<int, 0>{});
-        if (t + 1 >= ntiles) break;
-        iter(t + 1, std::integral_constant<int, 1>{});
-        if (t + 2 >= ntiles) break;
-        iter(t + 2, std::integral_constant<int, 2>{});
-        if (t + 3 >= ntiles) break;
-        iter(t + 3, std::integral_constant<int, 3>{});
-        if (t + 4 >= ntiles) break;
-        iter(t + 4, std::integral_constant<int, 4>{});
-        if (t + 5 >= ntiles) break;
-        iter(t + 5, std::integral_constant<int, 5>{});
-      }
-    }
-    if (ntiles == 0) asm volatile("s_barrier" ::: "memory");
-    if (has_next) {
-      begin(vc, nit.row, nit.head);
-      if (nit.ntiles > 0) { Dma d = next_dma(vc, 1); WB::template dma_cs<1, 0>(r0, cx0, cx0, lw, d.last, d.ld2, d.base); }
-    }
-    // ---- epilogue of this item, per 32-query block, rows straight from the accumulator layout (attn_pack_out's
-    // order: gate loads in flight while O is read out and packed; attn_pack_o's layout, per dt)
-#pragma unroll
-    for (int J = 0; J < 2; ++J) {
-      const float inv = 1.0f / halves_sum(J == 0 ? la : lb);
-      const int qi = cur.qw + 32 * J + ql;
-      const bool valid = qi < a.n_q;
-      if (!__any(valid)) continue;
-      const int qc = min(qi, a.n_q - 1);
-      uint4 v4[8];
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        float od[16];
-        if (J == 0) {
-          if (dt == 0) WB::get_o_0_0(od); else if (dt == 1) WB::get_o_0_1(od); else if (dt == 2) WB::get_o_0_2(od); else WB::get_o_0_3(od);
-        } else {
-          if (dt == 0) WB::get_o_1_0(od); else if (dt == 1) WB::get_o_1_1(od); else if (dt == 2) WB::get_o_1_2(od); else WB::get_o_1_3(od);
-        }
-        uint32_t wd[4][2];
-#pragma unroll
-        for (int rg = 0; rg < 4; ++rg) {
-          wd[rg][0] = pack2bf(rbf(od[4 * rg + 0] * inv), rbf(od[4 * rg + 1] * inv));
-          wd[rg][1] = pack2bf(rbf(od[4 * rg + 2] * inv), rbf(od[4 * rg + 3] * inv));
-        }
-#pragma unroll
-        for (int kx = 0; kx < 2; ++kx) {
-          const auto x = __builtin_amdgcn_permlane32_swap(wd[2 * kx][0], wd[2 * kx + 1][0], false, false);
-          const auto y = __builtin_amdgcn_permlane32_swap(wd[2 * kx][1], wd[2 * kx + 1][1], false, false);
-          v4[2 * dt + kx] = make_uint4(x[0], y[0], x[1], y[1]);
-        }
-      }
-      if (a.gate && valid) {
-        const bf16_t* gp = (const bf16_t*)a.gate + ECHO_QROW(a, cur.row) * a.g_ld_batch + (int64_t)qc * a.g_ld_tok +
-                           cur.head * 128 + 8 * h2;
-        uint4 g4[8];
-#pragma unroll
-        for (int pk = 0; pk < 8; ++pk) g4[pk] = *(const uint4*)(gp + 16 * pk);
-        attn_gate(v4, g4);
-      }
-      attn_write_out(v4, (bf16_t*)a.out + cur.row * a.o_ld_batch + (int64_t)qc * a.o_ld_tok + cur.head * 128, h2, valid);
-    }
-    if (!has_next) break;
-    WB::zero_o();
-    // the next item's Q, K(0..2), V(0) (and this item's stores) have landed in every wave
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    L = nxt;
-    cur = nit;
-  }
-}
-#pragma clang diagnostic pop
 
 // one (query qi, 8 output columns c8) unit of (row, head) rh of the split-KV combine
 template <class Args>
@@ -1685,16 +1394,6 @@ int attn_ps_grid(int nitems) {
   return min(nitems, (2 * cus + 7) / 8 * 8);
 }
 
-int cu_count_attn() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      return 256;
-    cus = n;
-  }
-  return cus;
-}
 
 // Measurement variants of the bf16 kernel (tools/bench_attn.py; DESIGN.md §7 lists what each
 // showed). variant: 0 production (4 waves, 2-slot LDS-DMA ring, 64-key tiles), 1/2 8 waves with
@@ -1710,6 +1409,12 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
 #define ECHO_ATTN_ABLS(NW, ST)                        \
   switch (abl) {                                      \
     case 0: ECHO_ATTN_LAUNCH(0, NW, ST); break;       \
+    case 128: ECHO_ATTN_LAUNCH(128, NW, ST); break;   \
+    ECHO_ATTN_DIAG_ABLS(NW, ST)                       \
+    default: return ECHO_EINVAL;                      \
+  }
+#ifdef ECHO_DIAG
+#define ECHO_ATTN_DIAG_ABLS(NW, ST)                   \
     case 1: ECHO_ATTN_LAUNCH(1, NW, ST); break;       \
     case 2: ECHO_ATTN_LAUNCH(2, NW, ST); break;       \
     case 3: ECHO_ATTN_LAUNCH(3, NW, ST); break;       \
@@ -1722,12 +1427,12 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 35: ECHO_ATTN_LAUNCH(35, NW, ST); break;     \
     case 51: ECHO_ATTN_LAUNCH(51, NW, ST); break;     \
     case 64: ECHO_ATTN_LAUNCH(64, NW, ST); break;     \
-    case 128: ECHO_ATTN_LAUNCH(128, NW, ST); break;   \
     case 256: ECHO_ATTN_LAUNCH(256, NW, ST); break;   \
     case 640: ECHO_ATTN_LAUNCH(640, NW, ST); break;   \
-    case 641: ECHO_ATTN_LAUNCH(641, NW, ST); break;   \
-    default: return ECHO_EINVAL;                      \
-  }
+    case 641: ECHO_ATTN_LAUNCH(641, NW, ST); break;
+#else
+#define ECHO_ATTN_DIAG_ABLS(NW, ST)
+#endif
   switch (cfg) {
     case 0: ECHO_ATTN_ABLS(4, 2); break;
     case 1: ECHO_ATTN_ABLS(8, 2); break;
@@ -1752,6 +1457,18 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       if (abl || any_causal(a)) return ECHO_EINVAL;
       hipLaunchKernelGGL(attn_pl_kernel<0>, grid, dim3(256), 0, s, *a);
       break;
+    case 30:  // one wave per SIMD, 64 queries per wave, two waves per workgroup (measured slower)
+      if (abl || any_causal(a)) return ECHO_EINVAL;
+      hipLaunchKernelGGL((attn_w64_kernel<0, 2>), grid, dim3(128), 0, s, *a);
+      break;
+    case 40:  // four waves x 64 queries (256-query workgroups)
+      if (abl || any_causal(a)) return ECHO_EINVAL;
+      hipLaunchKernelGGL((attn_w64_kernel<0, 4>), dim3(attn_grid(a, 256)), dim3(256), 0, s, *a);
+      break;
+#ifdef ECHO_DIAG
+    // ablations of the asm-owned kernels (timing only, results wrong; DESIGN.md §3 lists what each showed):
+    // attn_pl_kernel ABL bits 12-18, 8 waves x 32 queries 20-22, attn_w64_kernel 31-33 / 41-43 (16 no tile loop,
+    // 1 no loop DMA, 8 no end-of-tile wait)
     case 12: hipLaunchKernelGGL(attn_pl_kernel<1>, grid, dim3(256), 0, s, *a); break;
     case 13: hipLaunchKernelGGL(attn_pl_kernel<2>, grid, dim3(256), 0, s, *a); break;
     case 14: hipLaunchKernelGGL(attn_pl_kernel<4>, grid, dim3(256), 0, s, *a); break;
@@ -1759,31 +1476,21 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 16: hipLaunchKernelGGL(attn_pl_kernel<16>, grid, dim3(256), 0, s, *a); break;
     case 17: hipLaunchKernelGGL(attn_pl_kernel<6>, grid, dim3(256), 0, s, *a); break;
     case 18: hipLaunchKernelGGL(attn_pl_kernel<7>, grid, dim3(256), 0, s, *a); break;
-    case 30: case 31: case 32: case 33:  // one wave per SIMD, 64 queries per wave (31-33: ablations 16 no tile
-      // loop, 1 no loop DMA, 8 no end-of-tile wait)
+    case 31: case 32: case 33:
       if (any_causal(a)) return ECHO_EINVAL;
-      if (cfg == 30) hipLaunchKernelGGL((attn_w64_kernel<0, 2>), grid, dim3(128), 0, s, *a);
-      else if (cfg == 31) hipLaunchKernelGGL((attn_w64_kernel<16, 2>), grid, dim3(128), 0, s, *a);
+      if (cfg == 31) hipLaunchKernelGGL((attn_w64_kernel<16, 2>), grid, dim3(128), 0, s, *a);
       else if (cfg == 32) hipLaunchKernelGGL((attn_w64_kernel<1, 2>), grid, dim3(128), 0, s, *a);
       else hipLaunchKernelGGL((attn_w64_kernel<8, 2>), grid, dim3(128), 0, s, *a);
       break;
-    case 44: case 45: {  // persistent 4 waves x 64 queries (45: no tile loop), one workgroup per CU
-      if (any_causal(a)) return ECHO_EINVAL;
-      const int nit = attn_grid(a, 256), gp = min(nit, cu_count_attn());
-      if (cfg == 44) hipLaunchKernelGGL(attn_w64p_kernel<0>, dim3(gp), dim3(256), 0, s, *a);
-      else hipLaunchKernelGGL(attn_w64p_kernel<16>, dim3(gp), dim3(256), 0, s, *a);
-      break;
-    }
-    case 40: case 41: case 42: case 43: {  // 4 waves x 64 queries (256-query workgroups; 41-43: ablations as 31-33)
+    case 41: case 42: case 43: {
       if (any_causal(a)) return ECHO_EINVAL;
       const dim3 g4(attn_grid(a, 256));
-      if (cfg == 40) hipLaunchKernelGGL((attn_w64_kernel<0, 4>), g4, dim3(256), 0, s, *a);
-      else if (cfg == 41) hipLaunchKernelGGL((attn_w64_kernel<16, 4>), g4, dim3(256), 0, s, *a);
+      if (cfg == 41) hipLaunchKernelGGL((attn_w64_kernel<16, 4>), g4, dim3(256), 0, s, *a);
       else if (cfg == 42) hipLaunchKernelGGL((attn_w64_kernel<1, 4>), g4, dim3(256), 0, s, *a);
       else hipLaunchKernelGGL((attn_w64_kernel<8, 4>), g4, dim3(256), 0, s, *a);
       break;
     }
-    case 20: case 21: case 22: {  // asm pipeline at 8 waves x 32 queries (21: no tile loop, 22: no X / Y bodies)
+    case 20: case 21: case 22: {
       if (any_causal(a)) return ECHO_EINVAL;
       const dim3 g8(attn_grid(a, 256));
       if (cfg == 20) hipLaunchKernelGGL((attn_pl_kernel<0, 8>), g8, dim3(512), 0, s, *a);
@@ -1791,6 +1498,7 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       else hipLaunchKernelGGL((attn_pl_kernel<6, 8>), g8, dim3(512), 0, s, *a);
       break;
     }
+#endif
     default: return ECHO_EINVAL;
   }
 #undef ECHO_ATTN_ABLS

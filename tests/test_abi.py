@@ -247,3 +247,15 @@ def test_gemm_small_m_plan_host_policy(lib):
     assert planned(30720, 2048, 5888, 0) == lib.echo_gemm_pick_tile(30720, 2048, 5888, 1)
     assert lib.echo_attention_set_pipeline(3) != 0 and lib.echo_attention_set_pipeline(-1) != 0
     assert lib.echo_attention_set_pipeline(0) == 0 and lib.echo_attention_set_pipeline(1) == 0
+
+
+def test_asm_owned_attention_registers_untouched():
+    """hipcc never names a register the asm-owned attention bodies keep live across its code (the VGPR cap keeps it
+    out of the owned VGPRs, nothing but this check keeps it out of the owned AGPRs), and those kernels do not
+    spill (tools/check_owned_regs.py on the product build's gfx950 assembly)."""
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "tools", "check_owned_regs.py")],
+                       capture_output=True, text=True, timeout=600, env={**os.environ, "ECHO_DIAG": "0"})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert r.stdout.strip().endswith("0 violations")

@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Check that hipcc never touches the registers the hand-written attention bodies own.
 
-attn_pl_kernel owns v96..v255 (hipcc capped at 96 VGPRs), attn_w64_kernel / attn_w64p_kernel own v128..v255 and
+attn_pl_kernel owns v96..v255 (hipcc capped at 96 VGPRs), attn_w64_kernel owns v128..v255 and
 a0..a223 (hipcc capped at 128 VGPRs). The VGPR cap keeps hipcc out of the owned VGPRs, but nothing keeps it out
 of the AGPRs: under register pressure it spills VGPRs into AGPRs (v_accvgpr_write / read) between the asm
 statements, which would silently overwrite the O accumulators or Q fragments. This tool compiles attention.hip
-to gfx950 assembly and fails if any instruction OUTSIDE an inline-asm block of those kernels names an owned
+to gfx950 assembly (the product build; ECHO_DIAG=1 in the environment adds -DECHO_DIAG, the ablation instantiations) and fails if any instruction OUTSIDE an inline-asm block of those kernels names an owned
 register, or if the kernels spill to scratch.
 
     python tools/check_owned_regs.py [attention.s]
@@ -19,12 +19,13 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "echo-tts_amd", "csrc")
-KERNELS = {"attn_pl_kernel": (96, None), "attn_w64_kernel": (128, 224), "attn_w64p_kernel": (128, 224)}
+KERNELS = {"attn_pl_kernel": (96, None), "attn_w64_kernel": (128, 224)}
 
 
 def compile_asm(out):
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-           f"-I{os.path.join(REPO, 'include')}", "--cuda-device-only", "-S", os.path.join(CSRC, "attention.hip"),
+           f"-I{os.path.join(REPO, 'include')}", "--cuda-device-only",
+           *(["-DECHO_DIAG"] if os.environ.get("ECHO_DIAG") == "1" else []), "-S", os.path.join(CSRC, "attention.hip"),
            "-o", out]
     subprocess.run(cmd, check=True, capture_output=True)
 
@@ -42,16 +43,14 @@ def regs_in(line):
 def check(path):
     text = open(path).read()
     bad = []
-    for m in re.finditer(r"^(_Z\w*?(attn_pl_kernel|attn_w64p?_kernel)\w*):(\s*;.*)?$", text, re.M):
+    for m in re.finditer(r"^(_Z\w*?(attn_pl_kernel|attn_w64_kernel)\w*):(\s*;.*)?$", text, re.M):
         name, fam = m.group(1), m.group(2)
         vlo, alim = KERNELS[fam]
         end = text.index(".Lfunc_end", m.end())
         body = text[m.end():end].split("\n")
-        # attn_pl_kernel / attn_w64_kernel: owned state is dead after the kernel's last asm block (the final O
-        # read-out); attn_w64p_kernel loops over items (the next item's Q is live in the epilogue): strict everywhere
+        # owned state is dead after the kernel's last asm block (the final O read-out); a persistent form that keeps
+        # the next item's state live across its epilogue would have to be checked to the end
         last = max((i for i, ln in enumerate(body) if ";;#ASMEND" in ln), default=len(body))
-        if fam == "attn_w64p_kernel":
-            last = len(body)
         in_asm = False
         for li, ln in enumerate(body):
             if li > last:

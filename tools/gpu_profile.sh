@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box helper: rocprofv3 kernel-trace statistics of one bench workload, summarised on the box by
-# tools/trace_shapes.py (per kernel and launch shape; raw trace deleted so the copy-back stays small), and
+# tools/trace_shapes.py (per kernel and launch shape) and tools/layer_timeline.py (per decoder layer; raw trace deleted so the copy-back stays small), and
 # optionally FETCH_SIZE / WRITE_SIZE PMC passes (one counter per pass, kernel trace only, never combined with
 # runtime / system traces) over the path's kernels, tabulated by tools/pmc_table3.py.
 # usage: tools/gpu_profile.sh <tag> <c3|c2|c5|c5b1> [pmc]      outputs: gpurun_out/<tag>_<cfg>.*
@@ -21,6 +21,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$D" -o run --output-forma
   -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-extra $A > "$D.json" 2> "$D.err" || exit $?
 T=$(find "$D" -name '*kernel_trace.csv' | head -n 1)
 python3 "$R/tools/trace_shapes.py" "$T" --calls $CALLS > "$D.shapes.txt" 2>&1 || exit $?
+python3 "$R/tools/layer_timeline.py" "$T" > "$D.timeline.txt" 2>&1 || exit $?
 find "$D" -name '*kernel_trace.csv' -delete
 [ "$PMC" = pmc ] || exit 0
 KRE="(gemm_bf16|gemm_splitk|attn_|adaln|head_norm)"
