@@ -2,7 +2,7 @@
 # GPU-box helper: rocprofv3 kernel-trace statistics of one bench workload, summarised on the box by
 # tools/trace_shapes.py (per kernel and launch shape) and tools/layer_timeline.py (per decoder layer; raw trace deleted so the copy-back stays small), and
 # optionally FETCH_SIZE / WRITE_SIZE PMC passes (one counter per pass, kernel trace only, never combined with
-# runtime / system traces) over the path's kernels, tabulated by tools/pmc_table3.py.
+# runtime / system traces) over every kernel of the run, tabulated by tools/pmc_table3.py.
 # usage: tools/gpu_profile.sh <tag> <c3|c2|c5|c5b1> [pmc]      outputs: gpurun_out/<tag>_<cfg>.*
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -24,9 +24,8 @@ python3 "$R/tools/trace_shapes.py" "$T" --calls $CALLS > "$D.shapes.txt" 2>&1 ||
 python3 "$R/tools/layer_timeline.py" "$T" > "$D.timeline.txt" 2>&1 || exit $?
 find "$D" -name '*kernel_trace.csv' -delete
 [ "$PMC" = pmc ] || exit 0
-KRE="(gemm_bf16|gemm_splitk|attn_|adaln|head_norm)"
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 240 rocprofv3 --pmc $C --kernel-include-regex "$KRE" --output-format csv \
+  timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv \
     -d "$D.pmc/$C" -o pmc -- python3 "$R/bench.py" --no-graph --no-extra --no-cpu-baseline \
     --no-roofline --steps 2 --warmup 1 $A > "$D.pmc_$C.log" 2>&1 || exit $?
 done
