@@ -1559,11 +1559,11 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int grp = wid >> 2;  // ping-pong group: waves 4-7 run one barrier behind
-  constexpr int GM = 8;
-  // tile t -> origin: XCD-chunked (t & 7 = XCD) group-M order
+  // tile t -> origin: XCD-chunked (t & 7 = XCD) group-M order (GM rows of tiles per group: Epi::gm, default 8)
   auto origin = [&](int t, int& m0o, int& n0o) __attribute__((always_inline)) {
     KA* const kq = kargs();
     const int tiles_m = kq->tiles_m, tiles_n = kq->tiles_n;
+    const int GM = kq->ep.gm > 0 ? kq->ep.gm : 8;
     const int nwg = tiles_m * tiles_n;
     const int q8 = nwg >> 3, r8 = nwg & 7;
     const int xcd = t & 7;
@@ -2240,6 +2240,8 @@ int launch_pp2_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 
 int g_num_cus = 0;  // persistent grid size (hipDeviceProp multiProcessorCount, queried once)
 
+int g_gemm_group_m = 0;  // echo_gemm_set_diag key 13: group-M height of the persistent 256x256 and 320-row kernels (A/B)
+
 template <int EK>
 int launch_ps_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   const int tm = (a->M + 255) / 256, tn = (a->N + 255) / 256;
@@ -2256,7 +2258,7 @@ int launch_ps_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   // 2-6 % slower on QKVG/W13; on the N = 2048 residual GEMMs 4 was within +-2 % of 8 in either
   // direction across two boxes (Wo 245 vs 252 / 235 vs 229 us, W2 591 vs 604 / 579 vs 587 us)
   Epi e = ep;
-  if (e.gm <= 0) e.gm = 8;
+  if (e.gm <= 0) e.gm = g_gemm_group_m > 0 ? g_gemm_group_m : 8;
   hipLaunchKernelGGL((gemm_bf16_ps_kernel<EK>), dim3(grid, a->batch), dim3(512), 0, s, (const bf16_t*)a->A,
                      a->lda, a->stride_a, (const bf16_t*)a->W, a->ldw, a->stride_w, a->C, a->ldc, a->stride_c,
                      a->M, a->N, a->K, tm, tn, e);
@@ -2372,7 +2374,9 @@ int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
     const int cus = cu_count_cached() & ~7;
     if (cus >= 8 && grid > cus) grid = cus;
   }
-  const T320Args ta{(const bf16_t*)a->A, a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, ep};
+  Epi e2 = ep;
+  if (e2.gm <= 0) e2.gm = g_gemm_group_m > 0 ? g_gemm_group_m : 8;
+  const T320Args ta{(const bf16_t*)a->A, a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, e2};
   if (ek_of(a) == EK_SWIGLU)
     hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_SWIGLU, SP, PER>), dim3(grid), dim3(512), 0, s, ta);
   else if (ek_of(a) == EK_HEADNORM)
@@ -2633,6 +2637,7 @@ extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   else if (key == 9) g_adaln_blocks = value;
   else if (key == 11) g_gemm_no_splitk = value != 0;
   else if (key == 12) g_gemm_no_sk = value != 0;
+  else if (key == 13) { if (value < 0 || value > 64) return ECHO_EINVAL; g_gemm_group_m = value; }
   else return ECHO_EINVAL;
   return 0;
 }
