@@ -2240,7 +2240,10 @@ int launch_pp2_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 
 int g_num_cus = 0;  // persistent grid size (hipDeviceProp multiProcessorCount, queried once)
 
-int g_gemm_group_m = 0;  // echo_gemm_set_diag key 13: group-M height of the persistent 256x256 and 320-row kernels (A/B)
+// group-M height of the persistent 256x256 and 320-row kernels (echo_gemm_set_diag key 13; 0 = 4). Each XCD's
+// 32 concurrent tiles then cover 4 row panels x 8 column panels: 13.2 MB of A / W panels per XCD round for the
+// 320-row tiles (14.5 MB at 8 x 4) — C3 +0.7 % over 8, 16 -1.7 %, 2 / 3 / 5 / 6 between (profiles/r5_gemm_group_m.txt)
+int g_gemm_group_m = 0;
 
 template <int EK>
 int launch_ps_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
@@ -2258,7 +2261,7 @@ int launch_ps_ek(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   // 2-6 % slower on QKVG/W13; on the N = 2048 residual GEMMs 4 was within +-2 % of 8 in either
   // direction across two boxes (Wo 245 vs 252 / 235 vs 229 us, W2 591 vs 604 / 579 vs 587 us)
   Epi e = ep;
-  if (e.gm <= 0) e.gm = g_gemm_group_m > 0 ? g_gemm_group_m : 8;
+  if (e.gm <= 0) e.gm = g_gemm_group_m > 0 ? g_gemm_group_m : 4;
   hipLaunchKernelGGL((gemm_bf16_ps_kernel<EK>), dim3(grid, a->batch), dim3(512), 0, s, (const bf16_t*)a->A,
                      a->lda, a->stride_a, (const bf16_t*)a->W, a->ldw, a->stride_w, a->C, a->ldc, a->stride_c,
                      a->M, a->N, a->K, tm, tn, e);
@@ -2375,7 +2378,7 @@ int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
     if (cus >= 8 && grid > cus) grid = cus;
   }
   Epi e2 = ep;
-  if (e2.gm <= 0) e2.gm = g_gemm_group_m > 0 ? g_gemm_group_m : 8;
+  if (e2.gm <= 0) e2.gm = g_gemm_group_m > 0 ? g_gemm_group_m : 4;
   const T320Args ta{(const bf16_t*)a->A, a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm, tn, e2};
   if (ek_of(a) == EK_SWIGLU)
     hipLaunchKernelGGL((gemm_bf16_t320_kernel<EK_SWIGLU, SP, PER>), dim3(grid), dim3(512), 0, s, ta);
