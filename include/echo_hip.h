@@ -127,7 +127,8 @@ int echo_set_policy_rows(int32_t num, int32_t den);
  * (`tile` 22 / 23 force one 320-row tile per workgroup / the persistent 320-row kernel for any epilogue;
  * A/B timing, all bitwise-equal; key 10 is retired.)
  * key 11: 1 = never split K in echo_gemm_ws (the B = 1 runs that tests compare bitwise with B = 16 rows);
- * key 12: 1 = no small-M kernel in the auto pick (the round-3 small tiles; A/B).
+ * key 12: 1 = no small-M kernel in the auto pick (the round-3 small tiles; A/B);
+ * key 13: group-M height of the persistent 256x256 and 320-row kernels' tile order (0 = 4; 1..64; bitwise-equal).
  * `tile` 100 + 10*C + S (C = small-M config 1..16, S = split 1..9) forces a small-M launch (tools/bench_gemm.py). */
 int echo_gemm_set_diag(int32_t key, int32_t value);
 

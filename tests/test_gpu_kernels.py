@@ -205,6 +205,34 @@ def test_gemm_t320_bitwise(M, N, K):
         close_bf16(b[:, :N], ref)
 
 
+def test_gemm_group_m_order_bitwise():
+    """The group-M height of the persistent 256x256 and 320-row kernels (echo_gemm_set_diag key 13, default 4)
+    changes only which workgroup computes which tile and when: results bitwise equal for heights 1 / 2 / 4 / 8 / 16
+    on the 320-row persistent SwiGLU form, the 320-row gated residual and the persistent 256x256 kernel (a partial
+    last row of tiles included)."""
+    lib = L.load()
+    torch.manual_seed(13)
+    cases = [(10240, 11776, 512, L.EPI_SWIGLU, 23), (10240, 2048, 512, L.EPI_RESID, 20),
+             (1920, 2048, 512, L.EPI_STORE, 16), (1000, 11776, 256, L.EPI_SWIGLU, 16)]
+    try:
+        for M, N, K, epi, tile in cases:
+            a = torch.randn(M, K, device=DEV).to(BF)
+            w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+            h = torch.randn(M, N, device=DEV).to(BF)
+            outs = []
+            for gm in (0, 1, 2, 8, 16):
+                assert lib.echo_gemm_set_diag(13, gm) == 0
+                if epi == L.EPI_RESID:
+                    o = h.clone()
+                    ops.gemm(a, w, out=o, epilogue=epi, aux=o, tile=tile)
+                else:
+                    o = ops.gemm(a, w, epilogue=epi, tile=tile)
+                outs.append(o)
+            assert all(torch.equal(outs[0], o) for o in outs[1:]), (M, N, K, epi, tile)
+    finally:
+        lib.echo_gemm_set_diag(13, 0)
+
+
 @pytest.mark.parametrize("M,N,K", [(10240, 11776, 2048), (30720, 11776, 256), (640, 512, 128), (960, 768, 192)])
 def test_gemm_t320_swiglu_bitwise(M, N, K):
     """320x256 tiles with the SwiGLU epilogue (W13 at M = 30720 / 10240: the auto pick splits the columns,
