@@ -1,5 +1,5 @@
 """Under-filled compute-bound residual GEMMs (N = 2048: Wo K = 2048, W2 K = 5888) at the blockwise B = 16 and C2 row
-counts: the auto plan vs forced small-M configs, including the 256x256 8-wave config 17 with K split S, with the
+counts: the auto plan vs forced small-M configs (config 15 and 6 with K split S; round 5 also tried a 256x256 config), with the
 weights rotated over 8 copies (streamed from HBM as in the sampler). Also checks every forced unsplit config
 against the auto plan bitwise, and split configs within fp32-reordering distance.
 
@@ -50,7 +50,7 @@ def main():
         ref = h0.clone()
         ops.gemm(a, ws[0], out=ref, epilogue=L.EPI_RESID, aux=ref, gate=g, tile=13)
         line = [f"M{M} N{N} K{K}:"]
-        for tile in [0, 13, 251, 252, 253, 271, 272, 273, 274, 276]:
+        for tile in [0, 13, 251, 252, 253, 161, 162, 163, 164]:
             o = h0.clone()
             try:
                 ops.gemm(a, ws[0], out=o, epilogue=L.EPI_RESID, aux=o, gate=g, tile=tile)
