@@ -1553,7 +1553,8 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
   constexpr int BM = 320, BN = 256, TM = 80, TN = 128, FM = 5, FN = 8;
   constexpr int STAGE = (BM + BN) * BK;
   constexpr int SN = t320_sn(EK);
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+  // + the persistent head-norm form's norm weights: 128 per wave (its head), staged once per tile (2 KiB)
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE + ((EK == EK_HEADNORM && PER) ? 8 * 128 : 0)];
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1792,13 +1793,25 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
 #pragma unroll
           for (int j = 0; j < FN; ++j) asm volatile("" : "+v"(hpa[ii][j].x), "+v"(hpa[ii][j].y));
       }
-      // norm weights: PER re-reads them per row fragment (L1 hits) instead of holding 16 registers across the
-      // row loop (the persistent form's live range is what spilled)
+      // norm weights: PER stages the wave's 128 (one global load per lane, one latency per tile) in its own 256 B
+      // of LDS past the ring and reads them per row fragment, instead of holding 16 registers across the row
+      // loop (that live range spilled) or re-reading them from global memory per fragment (a load latency
+      // exposed five times per tile)
       const bf16_t* wp = (const bf16_t*)ep.hn_w + hblk * ep.hn_w_stride + hhd * 128 + 4 * g4;
       uint2 hw[FN];
+      bf16_t* const hwl = lds + 2 * STAGE + wid * 128;
       if (!PER && hnorm) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) hw[j] = *(const uint2*)(wp + j * 16);
+      }
+      if constexpr (PER) {
+        if (hnorm) {
+          const uint32_t wv = *(const uint32_t*)((const bf16_t*)ep.hn_w + hblk * ep.hn_w_stride + hhd * 128 + 2 * le);
+          *(uint32_t*)(hwl + 2 * le) = wv;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
       }
 #pragma unroll
       for (int ii = 0; ii < FM; ++ii) {
@@ -1816,7 +1829,7 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
         if constexpr (PER) {
           if (hnorm) {
 #pragma unroll
-            for (int j = 0; j < FN; ++j) hw[j] = *(const uint2*)(wp + j * 16);
+            for (int j = 0; j < FN; ++j) hw[j] = *(const uint2*)(hwl + 4 * g4 + j * 16);
           }
         }
         if (hnorm) {
