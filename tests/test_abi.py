@@ -252,10 +252,12 @@ def test_gemm_small_m_plan_host_policy(lib):
 def test_asm_owned_attention_registers_untouched():
     """hipcc never names a register the asm-owned attention bodies keep live across its code (the VGPR cap keeps it
     out of the owned VGPRs, nothing but this check keeps it out of the owned AGPRs), and those kernels do not
-    spill (tools/check_owned_regs.py on the product build's gfx950 assembly)."""
+    spill (tools/check_owned_regs.py on the gfx950 assembly of the diagnostics build, ECHO_DIAG=1: the product
+    kernels plus every timing-ablation instantiation, so the diagnostics build is compiled here too)."""
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, os.path.join(repo, "tools", "check_owned_regs.py")],
-                       capture_output=True, text=True, timeout=600, env={**os.environ, "ECHO_DIAG": "0"})
+    r = subprocess.run([sys.executable, os.path.join(repo, "tools", "check_owned_regs.py"), "--compile-to",
+                        "/tmp/echo_attention_check_diag.s"],
+                       capture_output=True, text=True, timeout=900, env={**os.environ, "ECHO_DIAG": "1"})
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert r.stdout.strip().endswith("0 violations")

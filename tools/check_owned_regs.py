@@ -8,7 +8,7 @@ statements, which would silently overwrite the O accumulators or Q fragments. Th
 to gfx950 assembly (the product build; ECHO_DIAG=1 in the environment adds -DECHO_DIAG, the ablation instantiations) and fails if any instruction OUTSIDE an inline-asm block of those kernels names an owned
 register, or if the kernels spill to scratch.
 
-    python tools/check_owned_regs.py [attention.s]
+    python tools/check_owned_regs.py [--compile-to FILE | FILE]
 """
 from __future__ import annotations
 
@@ -76,8 +76,17 @@ def check(path):
 
 
 def main():
-    path = sys.argv[1] if len(sys.argv) > 1 else "/tmp/echo_attention_check.s"
-    if len(sys.argv) <= 1:
+    # check_owned_regs.py                      compile attention.hip to /tmp/echo_attention_check.s and check it
+    # check_owned_regs.py --compile-to FILE    compile to FILE and check it
+    # check_owned_regs.py FILE                 check an existing assembly file
+    args = sys.argv[1:]
+    if args[:1] == ["--compile-to"]:
+        path = args[1]
+        compile_asm(path)
+    elif args:
+        path = args[0]
+    else:
+        path = "/tmp/echo_attention_check.s"
         compile_asm(path)
     bad = check(path)
     for name, why, s in bad[:40]:
