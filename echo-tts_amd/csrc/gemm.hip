@@ -2850,6 +2850,29 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
     const int n320 = (a->M / 320) * (a->N / 256), cus = cu_count_cached();
     if (g_gemm_t320 == 2 ? n320 >= cus : t320_pays(a, cus)) return launch_t320(a, ep, s);
   }
+  // SwiGLU at 1537..2048 rows (W13 of the B = 1 CFG step, M = 1920: 8 x 46 = 368 tiles, two rounds of the
+  // persistent 256x256 kernel): the first ⌊0.94 CUs / row tiles⌋ tile columns there (one round) and the rest on
+  // the small-M 128x256 8-wave config (one round of half tiles) — 98.8 -> 88.2 us (profiles/r5_colsplit.txt).
+  // Same K order per element: bitwise equal.
+  if (a->tile == 0 && !g_gemm_no_colsplit && !g_gemm_no_sk && a->batch == 1 && t == 16 && ek_of(a) == EK_SWIGLU &&
+      a->N % 256 == 0) {
+    const int tm = (a->M + 255) / 256, tn = a->N / 256, cus = cu_count_cached();
+    const int c1 = (int)(0.94 * cus) / tm;
+    if ((tm == 7 || tm == 8) && tm * tn > cus && tm * tn < 2 * cus && c1 > 0 && c1 < tn) {
+      const int n1 = c1 * 256;
+      EchoGemmArgs h = *a, r = *a;
+      h.N = n1;
+      h.tile = 16;
+      r.N = a->N - n1;
+      r.W = (const bf16_t*)a->W + (int64_t)n1 * a->ldw;
+      r.C = (bf16_t*)a->C + n1 / 2;
+      r.tile = 100 + 10 * 13 + 1;
+      if (sk_ok(&r)) {
+        const int rc = echo_gemm(&h, stream);
+        return rc ? rc : echo_gemm(&r, stream);
+      }
+    }
+  }
   int tail_cfg = 0;
   const int M1 = (a->tile == 0 && (t == 13 || t == 16) && a->batch == 1 && !headnorm && !g_gemm_no_rowsplit)
                      ? split_rows(a->M, a->N, &tail_cfg) : 0;

@@ -1024,6 +1024,24 @@ def test_gemm_no_store_past_m(epi):
         assert ran >= 3, (M, N, ran)
 
 
+@pytest.mark.parametrize("M", [1920, 1600, 2048])
+def test_gemm_swiglu_column_split_bitwise(M):
+    """W13 at the B = 1 CFG step's row counts: the auto pick runs the first tile columns on the persistent 256x256
+    kernel and the rest on the small-M 128x256 config (two launches); bitwise equal to one 2-phase launch (tile 13)
+    and to the forced persistent kernel, and nothing written past the output's columns or rows."""
+    N, K = 11776, 512
+    torch.manual_seed(M)
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    ref = ops.gemm(a, w, epilogue=L.EPI_SWIGLU, tile=13)
+    buf = torch.full((M + 2, N // 2 + 64), 7.0, device=DEV, dtype=BF)
+    ops.gemm(a, w, out=buf[:M, :N // 2], epilogue=L.EPI_SWIGLU)
+    torch.cuda.synchronize()
+    assert torch.equal(buf[:M, :N // 2], ref)
+    assert bool((buf[M:] == 7.0).all()) and bool((buf[:, N // 2:] == 7.0).all())
+    assert torch.equal(ops.gemm(a, w, epilogue=L.EPI_SWIGLU, tile=16), ref)
+
+
 def test_gemm_small_m_policy_rows():
     """echo_set_policy_rows: the split decision for a launch of M rows taken as for M * num / den rows —
     a rank holding 1 of 8 prompts splits K exactly like the one-process run of 8 prompts (here: not at
