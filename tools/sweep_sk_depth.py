@@ -1,0 +1,119 @@
+"""The small-M GEMM family at the B = 1 decoder shapes: the auto plan vs every config unsplit and the K splits of the
+likely ones (round 5 also ran trial configs 17-20 with deeper LDS rings — four / five K-tiles of LDS-DMA in flight
+instead of two / three, 128x128 / 64x128 / 128x64 tiles, 144-160 KB — all slower; removed), with the weights
+rotated over 8 copies (streamed from HBM as in the sampler), a 300-launch warm-up (clock ramp) and the timed
+launches replayed from a graph. Forced
+unsplit configs are checked bitwise against the auto plan's unsplit result; split ones report the max |diff|.
+
+    python tools/sweep_sk_depth.py [shape ...]      shapes: w13 qkvg wo w2 (default all)
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import echo_tts_amd  # noqa: E402,F401
+from echo_tts_amd import _lib as L  # noqa: E402
+from echo_tts_amd import ops  # noqa: E402
+from echo_tts_amd.model import MAX_POS, rope_table_cpu  # noqa: E402
+
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def timed(fn, iters=24, rounds=7, reps=4):
+    """Median per-launch time of `iters` launches captured in one graph (no host launch overhead in the timing:
+    eager Python launches of these 10-30 us kernels are host-bound)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for i in range(iters):
+            fn(i)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(iters):
+            fn(i)
+    g.replay()
+    torch.cuda.synchronize()
+    res = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        res.append(e0.elapsed_time(e1) * 1e3 / (iters * reps))
+    return sorted(res)[len(res) // 2]
+
+
+# (name, N, K, epilogue, tiles to force per row count)
+ALL1 = [100 + 10 * c + 1 for c in range(1, 17)]
+SPLIT = [100 + 10 * c + S for c in (1, 3, 5, 6, 8, 9, 13) for S in (2, 3, 4)]
+SHAPES = {  # tile 100 + 10 c + S
+    "w13": (11776, 2048, "swiglu", {160: ALL1 + SPLIT, 480: ALL1 + SPLIT, 640: ALL1}),
+    "qkvg": (8192, 2048, "headnorm", {160: ALL1 + SPLIT, 480: ALL1 + SPLIT, 640: ALL1}),
+    "wo": (2048, 2048, "resid", {160: ALL1 + SPLIT, 480: ALL1 + SPLIT, 640: ALL1 + SPLIT}),
+    "w2": (2048, 5888, "resid", {160: ALL1 + SPLIT, 480: ALL1 + SPLIT, 640: ALL1 + SPLIT}),
+}
+
+
+def main():
+    torch.manual_seed(0)
+    names = sys.argv[1:] or list(SHAPES)
+    H = 16
+    qk = (1 + 0.1 * torch.randn(2, H, 128, device=DEV)).to(BF)
+    rope = rope_table_cpu(128, MAX_POS).to(DEV)
+    for name in names:
+        N, K, kind, per_m = SHAPES[name]
+        ws = [(torch.randn(N, K, device=DEV) * 0.02).to(BF) for _ in range(8)]
+        g = (torch.rand(N, device=DEV) + 0.5).to(BF)
+        for M, tiles in per_m.items():
+            a = torch.randn(M, K, device=DEV).to(BF)
+            nout = N // 2 if kind == "swiglu" else N
+            h0 = torch.randn(M, nout, device=DEV).to(BF)
+            outs = [h0.clone() for _ in range(8)]
+            hn = ops.HeadNorm(qk, H, 2, 1e-5, w_stride=H * 128, rope=rope, rope_heads=H // 2, seq_len=M,
+                              pos0=0) if kind == "headnorm" else None
+
+            def run(tile):
+                def f(i):
+                    o = outs[i % 8]
+                    if kind == "swiglu":
+                        ops.gemm(a, ws[i % 8], out=o, epilogue=L.EPI_SWIGLU, tile=tile)
+                    elif kind == "headnorm":
+                        ops.gemm(a, ws[i % 8], out=o, head_norm=hn, tile=tile)
+                    else:
+                        ops.gemm(a, ws[i % 8], out=o, epilogue=L.EPI_RESID, aux=o, gate=g, tile=tile)
+                return f
+
+            def result(tile):
+                o = h0.clone()
+                outs[0] = o
+                run(tile)(0)
+                torch.cuda.synchronize()
+                r = o.clone()
+                outs[0] = h0.clone()
+                return r
+
+            ref = result(0)
+            for i in range(300):
+                run(0)(i)
+            torch.cuda.synchronize()
+            line = [f"{name} M{M} N{N} K{K}: auto {timed(run(0)):6.1f}us"]
+            for t in tiles:
+                try:
+                    r = result(t)
+                except RuntimeError:
+                    continue
+                eq = "=" if torch.equal(r, ref) else f"~{(r.float() - ref.float()).abs().max().item():.1e}"
+                line.append(f"t{t} {timed(run(t)):5.1f}{eq}")
+            line.append(f"auto {timed(run(0)):6.1f}us")
+            print("  ".join(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
