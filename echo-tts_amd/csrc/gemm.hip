@@ -2791,7 +2791,14 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
   int t = a->tile > 0 ? a->tile : pick_tile(a->M, a->N, a->K, a->batch);
   // 256x256 tiles run the persistent 2-phase kernel where its register epilogue applies, else the
   // 2-phase ping-pong (all bitwise-identical results)
-  if (a->tile == 0 && t == 1) t = (a->dtype == ECHO_BF16 && ps_ok(a, ek_of(a)) && !g_gemm_no_ps) ? 16 : 13;
+  // Head norm in at most one tile round (the C2 CFG step's QKVG, M = 1920: 256 tiles): the 2-phase kernel with its
+  // LDS-staged epilogue, 63.3 -> 60.7 us against the persistent kernel's register epilogue, which gains nothing
+  // from persistence in one round (launches replayed from a graph, profiles/r5_sk_1920_sweep.txt; bitwise equal)
+  if (a->tile == 0 && t == 1) {
+    const int64_t tiles = (int64_t)((a->M + 255) / 256) * ((a->N + 255) / 256) * a->batch;
+    const bool one_round_hn = headnorm && tiles <= cu_count_cached();
+    t = (a->dtype == ECHO_BF16 && ps_ok(a, ek_of(a)) && !g_gemm_no_ps && !one_round_hn) ? 16 : 13;
+  }
   // fused on the persistent kernel (t 16/17/18, N % 256 == 0, via ps_ok) or the 2-phase one (t 13)
   const bool hn_fused = a->dtype == ECHO_BF16 && ((t == 13 && a->N % 128 == 0) ||
                                                    ((t == 16 || t == 18) && ps_ok(a, EK_HEADNORM)) ||

@@ -5,7 +5,8 @@ rotated over 8 copies (streamed from HBM as in the sampler), a 300-launch warm-u
 launches replayed from a graph. Forced
 unsplit configs are checked bitwise against the auto plan's unsplit result; split ones report the max |diff|.
 
-    python tools/sweep_sk_depth.py [shape ...]      shapes: w13 qkvg wo w2 (default all)
+    python tools/sweep_sk_depth.py [1920|big] [shape ...]   shapes: w13 qkvg wo w2 (default all); 1920: the C2 CFG rows;
+    big: 480 / 640 rows against the large-tile configs
 """
 import os
 import sys
@@ -59,16 +60,33 @@ SHAPES = {  # tile 100 + 10 c + S
     "wo": (2048, 2048, "resid", {160: ALL1 + SPLIT, 480: ALL1 + SPLIT, 640: ALL1 + SPLIT}),
     "w2": (2048, 5888, "resid", {160: ALL1 + SPLIT, 480: ALL1 + SPLIT, 640: ALL1 + SPLIT}),
 }
+BIG = [1, 2, 3, 4, 5, 13, 16, 20, 22, 23]
+SHAPES_1920 = {  # the C2 CFG step: large-tile configs too
+    "w13": (11776, 2048, "swiglu", {1920: BIG + ALL1}),
+    "qkvg": (8192, 2048, "headnorm", {1920: BIG + ALL1}),
+    "wo": (2048, 2048, "resid", {1920: BIG + ALL1 + SPLIT}),
+    "w2": (2048, 5888, "resid", {1920: BIG + ALL1 + SPLIT}),
+}
+SHAPES_BIG = {  # the small-M row counts against the large-tile configs
+    "w13": (11776, 2048, "swiglu", {480: BIG, 640: BIG}),
+    "qkvg": (8192, 2048, "headnorm", {480: BIG, 640: BIG}),
+    "wo": (2048, 2048, "resid", {480: BIG, 640: BIG}),
+    "w2": (2048, 5888, "resid", {480: BIG, 640: BIG}),
+}
 
 
 def main():
     torch.manual_seed(0)
-    names = sys.argv[1:] or list(SHAPES)
+    args = sys.argv[1:]
+    table = SHAPES
+    if args and args[0] in ("1920", "big"):
+        table, args = (SHAPES_1920 if args[0] == "1920" else SHAPES_BIG), args[1:]
+    names = args or list(table)
     H = 16
     qk = (1 + 0.1 * torch.randn(2, H, 128, device=DEV)).to(BF)
     rope = rope_table_cpu(128, MAX_POS).to(DEV)
     for name in names:
-        N, K, kind, per_m = SHAPES[name]
+        N, K, kind, per_m = table[name]
         ws = [(torch.randn(N, K, device=DEV) * 0.02).to(BF) for _ in range(8)]
         g = (torch.rand(N, device=DEV) + 0.5).to(BF)
         for M, tiles in per_m.items():
