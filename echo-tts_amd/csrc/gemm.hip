@@ -1627,7 +1627,8 @@ __global__ void __launch_bounds__(512) gemm_bf16_t320_kernel(T320Args args) {
   // tile k+1 (4 pieces), phase 1 cA of tile k+2 (5) instead of 2 / 7; cW0 then has one phase of DMA latency
   // instead of two. Waits: phase 0 retires cW1(k) -> vmcnt(9) (cA(k+1) 5 + this phase's 4 younger), phase 1
   // retires cA(k+1) + cW0(k+1) -> vmcnt(7). Measured within +-1 % of the 2 / 7 schedule on every decoder
-  // shape (profiles/r3_gemm_t320_dma_balance.txt): SP = 0 stays the default.
+  // shape (profiles/r3_gemm_t320_dma_balance.txt); round 5, replayed from graphs: -1 / -2 % for the gated residual
+  // at 3 tiles per CU (Wo / W2 at M = 30720), production there (launch_t320).
   // prologue: tile 0 (cA, cW0, then cW1) and cA (SP) or cA + cW0 (!SP) of tile 1; the tile loop's first wait
   // retires tile 0's cA + cW0 (PER: the previous tile's SN stores are younger and stay in flight)
   auto prologue = [&]() __attribute__((always_inline)) {
@@ -2408,11 +2409,14 @@ int launch_t320_sp(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 // (M = 7680: 2 tiles per CU, C5 -0.4 % when persistent) and the gated residual (3 / 1 tiles per CU, K = 5888 for
 // W2: no measurable gain). The head-norm epilogue's persistent form (spill-free since round 4: norm weights
 // and RoPE rows read at the use) from 8 tiles per CU: QKVG M = 30720 (12 per CU) 764.6 -> 753.0 us, M = 10240
-// (4 per CU) 258.5 vs 258.7 (profiles/r4_t320_headnorm_persistent.txt).
+// (4 per CU) 258.5 vs 258.7 (profiles/r4_t320_headnorm_persistent.txt). The gated residual from 2 tiles per CU
+// (Wo / W2 at M = 30720: 3 per CU) with the 4 / 5 DMA split (SP = 1): 212.1 -> 209.9 / 512.9 -> 502.9 us, launches
+// replayed from a graph, twice; at one round no difference (profiles/r5_sk_large_sweep.txt).
 int launch_t320(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   const int64_t tiles = (int64_t)(a->M / 320) * (a->N / 256), cus = cu_count_cached();
   const int ek = ek_of(a);
   const bool per = ((ek == EK_SWIGLU && tiles >= 4 * cus) || (ek == EK_HEADNORM && tiles >= 8 * cus));
+  if (!per && ek == EK_RESID && tiles >= 2 * cus) return launch_t320_sp<1, 0>(a, ep, s);
   return per ? launch_t320_sp<0, 1>(a, ep, s) : launch_t320_sp<0, 0>(a, ep, s);
 }
 

@@ -6,7 +6,7 @@ launches replayed from a graph. Forced
 unsplit configs are checked bitwise against the auto plan's unsplit result; split ones report the max |diff|.
 
     python tools/sweep_sk_depth.py [1920|big] [shape ...]   shapes: w13 qkvg wo w2 (default all); 1920: the C2 CFG rows;
-    big: 480 / 640 rows against the large-tile configs
+    big: 480 / 640 rows against the large-tile configs; large: the C3 and blockwise B = 16 row counts
 """
 import os
 import sys
@@ -67,6 +67,13 @@ SHAPES_1920 = {  # the C2 CFG step: large-tile configs too
     "wo": (2048, 2048, "resid", {1920: BIG + ALL1 + SPLIT}),
     "w2": (2048, 5888, "resid", {1920: BIG + ALL1 + SPLIT}),
 }
+BIG2 = [1, 2, 3, 13, 16, 20, 21, 22, 23]
+SHAPES_LARGE = {  # C3 (48 / 16 rows x 640) and blockwise B = 16 (2560 / 7680) row counts
+    "w13": (11776, 2048, "swiglu", {30720: BIG2, 10240: BIG2, 2560: BIG2 + [231], 7680: BIG2}),
+    "qkvg": (8192, 2048, "headnorm", {30720: BIG2, 10240: BIG2, 2560: BIG2, 7680: BIG2}),
+    "wo": (2048, 2048, "resid", {30720: BIG2, 10240: BIG2, 2560: BIG2 + [251, 161], 7680: BIG2 + [251]}),
+    "w2": (2048, 5888, "resid", {30720: BIG2, 10240: BIG2, 2560: BIG2 + [251, 161], 7680: BIG2 + [251]}),
+}
 SHAPES_BIG = {  # the small-M row counts against the large-tile configs
     "w13": (11776, 2048, "swiglu", {480: BIG, 640: BIG}),
     "qkvg": (8192, 2048, "headnorm", {480: BIG, 640: BIG}),
@@ -79,8 +86,9 @@ def main():
     torch.manual_seed(0)
     args = sys.argv[1:]
     table = SHAPES
-    if args and args[0] in ("1920", "big"):
-        table, args = (SHAPES_1920 if args[0] == "1920" else SHAPES_BIG), args[1:]
+    if args and args[0] in ("1920", "big", "large"):
+        table = {"1920": SHAPES_1920, "big": SHAPES_BIG, "large": SHAPES_LARGE}[args[0]]
+        args = args[1:]
     names = args or list(table)
     H = 16
     qk = (1 + 0.1 * torch.randn(2, H, 128, device=DEV)).to(BF)
@@ -94,7 +102,7 @@ def main():
             nout = N // 2 if kind == "swiglu" else N
             h0 = torch.randn(M, nout, device=DEV).to(BF)
             outs = [h0.clone() for _ in range(8)]
-            hn = ops.HeadNorm(qk, H, 2, 1e-5, w_stride=H * 128, rope=rope, rope_heads=H // 2, seq_len=M,
+            hn = ops.HeadNorm(qk, H, 2, 1e-5, w_stride=H * 128, rope=rope, rope_heads=H // 2, seq_len=min(M, 640),
                               pos0=0) if kind == "headnorm" else None
 
             def run(tile):
