@@ -6,7 +6,8 @@ launches replayed from a graph. Forced
 unsplit configs are checked bitwise against the auto plan's unsplit result; split ones report the max |diff|.
 
     python tools/sweep_sk_depth.py [1920|big] [shape ...]   shapes: w13 qkvg wo w2 (default all); 1920: the C2 CFG rows;
-    big: 480 / 640 rows against the large-tile configs; large: the C3 and blockwise B = 16 row counts
+    big: 480 / 640 rows against the large-tile configs; large: the C3 and blockwise B = 16 row counts;
+    gm: the auto plan at each group-M height of the persistent tile orders
 """
 import os
 import sys
@@ -74,6 +75,13 @@ SHAPES_LARGE = {  # C3 (48 / 16 rows x 640) and blockwise B = 16 (2560 / 7680) r
     "wo": (2048, 2048, "resid", {30720: BIG2, 10240: BIG2, 2560: BIG2 + [251, 161], 7680: BIG2 + [251]}),
     "w2": (2048, 5888, "resid", {30720: BIG2, 10240: BIG2, 2560: BIG2 + [251, 161], 7680: BIG2 + [251]}),
 }
+GMS = [1, 2, 3, 4, 6, 8, 16]
+SHAPES_GM = {  # auto plan vs the group-M height of the persistent 256x256 / 320-row tile orders (diag key 13)
+    "w13": (11776, 2048, "swiglu", {30720: [], 10240: [], 7680: [], 2560: [], 1920: []}),
+    "qkvg": (8192, 2048, "headnorm", {30720: [], 10240: [], 7680: [], 2560: []}),
+    "wo": (2048, 2048, "resid", {30720: [], 10240: [], 7680: []}),
+    "w2": (2048, 5888, "resid", {30720: [], 10240: [], 7680: []}),
+}
 SHAPES_BIG = {  # the small-M row counts against the large-tile configs
     "w13": (11776, 2048, "swiglu", {480: BIG, 640: BIG}),
     "qkvg": (8192, 2048, "headnorm", {480: BIG, 640: BIG}),
@@ -86,8 +94,9 @@ def main():
     torch.manual_seed(0)
     args = sys.argv[1:]
     table = SHAPES
-    if args and args[0] in ("1920", "big", "large"):
-        table = {"1920": SHAPES_1920, "big": SHAPES_BIG, "large": SHAPES_LARGE}[args[0]]
+    gm_mode = bool(args) and args[0] == "gm"
+    if args and args[0] in ("1920", "big", "large", "gm"):
+        table = {"1920": SHAPES_1920, "big": SHAPES_BIG, "large": SHAPES_LARGE, "gm": SHAPES_GM}[args[0]]
         args = args[1:]
     names = args or list(table)
     H = 16
@@ -130,6 +139,14 @@ def main():
                 run(0)(i)
             torch.cuda.synchronize()
             line = [f"{name} M{M} N{N} K{K}: auto {timed(run(0)):6.1f}us"]
+            if gm_mode:
+                for gm in GMS:
+                    assert ops.lib().echo_gemm_set_diag(13, gm) == 0
+                    try:
+                        eq = "=" if torch.equal(result(0), ref) else "!"
+                        line.append(f"gm{gm} {timed(run(0)):6.1f}{eq}")
+                    finally:
+                        assert ops.lib().echo_gemm_set_diag(13, 0) == 0
             for t in tiles:
                 try:
                     r = result(t)
