@@ -24,6 +24,23 @@ def timeit(fn, iters=10, rounds=5):
     return sorted(ts)[len(ts) // 2]
 
 
+def gtimeit(fn, iters=10, rounds=5, reps=3):
+    """timeit with the launches replayed from a graph (the 15-40 us B = 1 launches are host-paced eagerly)."""
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        fn()
+    torch.cuda.current_stream().wait_stream(st)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    return timeit(g.replay, iters=reps, rounds=rounds) / iters
+
+
 def main():
     import argparse
     ap = argparse.ArgumentParser()
@@ -38,6 +55,7 @@ def main():
     ap.add_argument("--splits", default=None,
                     help="comma list of forced split-KV counts (1 = unsplit) for the production op: interleaved "
                          "rounds, median per count")
+    ap.add_argument("--graph", action="store_true", help="--splits: time launches replayed from a graph")
     args = ap.parse_args()
     dev = "cuda"
     B, N, H, T, P = args.batch, args.nq, 16, 448, 160
@@ -85,7 +103,7 @@ def main():
                     for c in counts:
                         with ops.attention_split(c):
                             f()
-                            tm[c].append(timeit(f, rounds=1))
+                            tm[c].append(gtimeit(f, rounds=1) if args.graph else timeit(f, rounds=1))
                 line = "  ".join(f"s{c} {sorted(v)[3] * 1e3:7.1f}" for c, v in tm.items())
                 print(f"R={R:3d} {name:10s} us by split: {line}", flush=True)
                 continue
