@@ -2545,9 +2545,10 @@ bool sk_plan(const EchoGemmArgs* a, bool allow_split, int* cfg, int* split) {
   const bool longk = a->K >= 4096;
   int c, S = 1;
   if (ek == EK_RESID && a->N >= 1024 && a->N <= 2048) {
-    // (M <= 256, K 5888: config 3 instead of 5 at S = 4 since round 5, the same K ranges and partial-sum order:
-    // 16.6 -> 15.9 us replayed from a graph, bitwise equal; profiles/r5_sk_depth_sweep.txt)
-    if (Mp <= 256) { c = longk ? 3 : 8; S = longk ? 4 : 2; }
+    // (M <= 256, K 5888: config 3 at S = 4 measured 16.6 -> 15.9 us in isolation, replayed from a graph with the
+    // activations L2-resident, but 19.0 -> 21.0 us with its finish inside the sampler, where the activations were
+    // just written: 64x64 tiles read them from the fabric twice as often; profiles/r5_sk_depth_sweep.txt)
+    if (Mp <= 256) { c = longk ? 5 : 8; S = longk ? 4 : 2; }
     else if (Mp <= 512) { c = longk ? 6 : 8; S = longk ? 4 : 1; }
     else if (Mp <= 768) { c = longk ? 6 : 3; S = longk ? 3 : 1; }
     else if (Mp <= 2048 && longk) c = 6;
