@@ -2,7 +2,8 @@
 likely ones (round 5 also ran trial configs 17-20 with deeper LDS rings — four / five K-tiles of LDS-DMA in flight
 instead of two / three, 128x128 / 64x128 / 128x64 tiles, 144-160 KB — all slower; removed), with the weights
 rotated over 8 copies (streamed from HBM as in the sampler), a 300-launch warm-up (clock ramp) and the timed
-launches replayed from a graph. Forced
+launches replayed from a graph. --fresh rewrites the activations with a copy kernel before every launch (the sampler
+hands each GEMM activations just written on other XCDs; times then include the copy, printed alone). Forced
 unsplit configs are checked bitwise against the auto plan's unsplit result; split ones report the max |diff|.
 
     python tools/sweep_sk_depth.py [1920|big] [shape ...]   shapes: w13 qkvg wo w2 (default all); 1920: the C2 CFG rows;
@@ -93,6 +94,8 @@ SHAPES_BIG = {  # the small-M row counts against the large-tile configs
 def main():
     torch.manual_seed(0)
     args = sys.argv[1:]
+    fresh = "--fresh" in args  # rewrite the activations before every launch (a copy kernel), as in the sampler
+    args = [v for v in args if v != "--fresh"]
     table = SHAPES
     gm_mode = bool(args) and args[0] == "gm"
     if args and args[0] in ("1920", "big", "large", "gm"):
@@ -108,6 +111,7 @@ def main():
         g = (torch.rand(N, device=DEV) + 0.5).to(BF)
         for M, tiles in per_m.items():
             a = torch.randn(M, K, device=DEV).to(BF)
+            asrc = [a.clone(), torch.randn(M, K, device=DEV).to(BF)]
             nout = N // 2 if kind == "swiglu" else N
             h0 = torch.randn(M, nout, device=DEV).to(BF)
             outs = [h0.clone() for _ in range(8)]
@@ -117,6 +121,8 @@ def main():
             def run(tile):
                 def f(i):
                     o = outs[i % 8]
+                    if fresh:
+                        a.copy_(asrc[i % 2])
                     if kind == "swiglu":
                         ops.gemm(a, ws[i % 8], out=o, epilogue=L.EPI_SWIGLU, tile=tile)
                     elif kind == "headnorm":
@@ -139,6 +145,8 @@ def main():
                 run(0)(i)
             torch.cuda.synchronize()
             line = [f"{name} M{M} N{N} K{K}: auto {timed(run(0)):6.1f}us"]
+            if fresh:
+                line.append(f"(copy alone {timed(lambda i: a.copy_(asrc[i % 2])):4.1f})")
             if gm_mode:
                 for gm in GMS:
                     assert ops.lib().echo_gemm_set_diag(13, gm) == 0
