@@ -113,6 +113,7 @@ ABI_VERSION = 6  # include/echo_hip.h ECHO_ABI_VERSION
 ABI_STRUCTS = {0: "GemmArgs", 1: "AttnArgs", 2: "KVSegment", 3: "StepArgs", 4: "RvqWeights"}
 
 _lib = None
+DIAG_APPLIED = {}  # echo_gemm_set_diag key -> value applied from ECHO_GEMM_DIAG at load (ops._KNOBS seeds from it)
 
 
 def load(path: str = LIB_PATH) -> C.CDLL:
@@ -134,6 +135,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         k, v = (int(x) for x in kv.split("="))
         if lib.echo_gemm_set_diag(k, v) != 0:
             raise RuntimeError(f"ECHO_GEMM_DIAG: echo_gemm_set_diag({k}, {v}) failed")
+        DIAG_APPLIED[k] = v
     return lib
 
 

@@ -945,6 +945,8 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
 // attn_bf16_kernel<0, 4, 2>'s (the deferred-max decision is taken per block, as there): bitwise equal.
 // Non-causal launches only. ABL (timing ablations, results wrong): 1 = no DMA in the tile loop, 8 = no end-of-tile
 // DMA wait (the barrier stays), 16 = no tile loop.
+// Measured slower than attn_pl_kernel: diagnostics build only (ECHO_DIAG=1), the product ABI refuses it.
+#ifdef ECHO_DIAG
 #include "attn_w64.inc"
 
 template <int ABL, int NW>
@@ -1199,7 +1201,7 @@ __global__ void __launch_bounds__(64 * NW, 1) __attribute__((amdgpu_num_vgpr(128
   store_block(std::integral_constant<int, 0>{}, la);
   store_block(std::integral_constant<int, 1>{}, lb);
 }
-
+#endif  // ECHO_DIAG
 
 // one (query qi, 8 output columns c8) unit of (row, head) rh of the split-KV combine
 template <class Args>
@@ -1382,6 +1384,7 @@ bool any_causal(const EchoAttnArgs* a) {
 
 int g_attn_pl = 1;  // echo_attention_set_pipeline: 0 = attn_bf16_kernel for every launch (A/B)
 
+#ifdef ECHO_DIAG
 // persistent grid: two workgroups per CU (a multiple of 8, so an item's XCD is its block's XCD)
 int attn_ps_grid(int nitems) {
   static int cus = 0;
@@ -1393,28 +1396,41 @@ int attn_ps_grid(int nitems) {
   }
   return min(nitems, (2 * cus + 7) / 8 * 8);
 }
+#endif
 
 
 // Measurement variants of the bf16 kernel (tools/bench_attn.py; DESIGN.md §7 lists what each
-// showed). variant: 0 production (4 waves, 2-slot LDS-DMA ring, 64-key tiles), 1/2 8 waves with
-// a 2/3-slot ring, 3/4 register-staged K/V with 4/8 waves, 5 software-pipelined kernel (two waves
-// per SIMD), 6/7 32-key tiles with a 2/3-slot ring, 8 the persistent form of 0, 9 two waves
-// (64 queries) per workgroup, 10 = 0 with the per-lane epilogue (round-2 form before the row-layout
-// epilogue). ablation: the ABL bits of attn_bf16_kernel.
+// showed). The product library keeps variant 0 (the compiler-scheduled production kernel, the bitwise
+// reference of the others) and 11 (attn_pl_kernel, production for non-causal launches) with ablation 0;
+// everything else is in the diagnostics build only (ECHO_DIAG=1) and refused with ECHO_EINVAL here:
+// 1/2 8 waves with a 2/3-slot ring, 3/4 register-staged K/V with 4/8 waves, 6/7 32-key tiles with a
+// 2/3-slot ring, 8 the persistent form of 0, 9 two waves (64 queries) per workgroup, 10 = 0 with the
+// per-lane epilogue (round-2 form before the row-layout epilogue), 30/40 attn_w64_kernel, the ablation
+// bits of attn_bf16_kernel (128: s_memrealtime stamps) and the asm kernels' ablations 12-22 / 31-43.
 int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) {
   const int qb = (cfg == 1 || cfg == 2 || cfg == 4) ? 256 : 128;
   const dim3 grid(attn_grid(a, qb));
+  if (cfg == 0 && abl == 0) {
+    hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1);
+    ECHO_LAUNCH_CHECK();
+    return 0;
+  }
+  if (cfg == 11) {  // asm-owned software pipeline (production for non-causal launches)
+    if (abl || any_causal(a)) return ECHO_EINVAL;
+    hipLaunchKernelGGL(attn_pl_kernel<0>, grid, dim3(256), 0, s, *a);
+    ECHO_LAUNCH_CHECK();
+    return 0;
+  }
+#ifndef ECHO_DIAG
+  (void)qb;
+  return ECHO_EINVAL;
+#else
 #define ECHO_ATTN_LAUNCH(A, NW, ST, ...) \
   hipLaunchKernelGGL((attn_bf16_kernel<A, NW, ST, ##__VA_ARGS__>), grid, dim3(64 * NW), 0, s, *a, (float*)nullptr, 1)
 #define ECHO_ATTN_ABLS(NW, ST)                        \
   switch (abl) {                                      \
     case 0: ECHO_ATTN_LAUNCH(0, NW, ST); break;       \
     case 128: ECHO_ATTN_LAUNCH(128, NW, ST); break;   \
-    ECHO_ATTN_DIAG_ABLS(NW, ST)                       \
-    default: return ECHO_EINVAL;                      \
-  }
-#ifdef ECHO_DIAG
-#define ECHO_ATTN_DIAG_ABLS(NW, ST)                   \
     case 1: ECHO_ATTN_LAUNCH(1, NW, ST); break;       \
     case 2: ECHO_ATTN_LAUNCH(2, NW, ST); break;       \
     case 3: ECHO_ATTN_LAUNCH(3, NW, ST); break;       \
@@ -1429,10 +1445,9 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
     case 64: ECHO_ATTN_LAUNCH(64, NW, ST); break;     \
     case 256: ECHO_ATTN_LAUNCH(256, NW, ST); break;   \
     case 640: ECHO_ATTN_LAUNCH(640, NW, ST); break;   \
-    case 641: ECHO_ATTN_LAUNCH(641, NW, ST); break;
-#else
-#define ECHO_ATTN_DIAG_ABLS(NW, ST)
-#endif
+    case 641: ECHO_ATTN_LAUNCH(641, NW, ST); break;   \
+    default: return ECHO_EINVAL;                      \
+  }
   switch (cfg) {
     case 0: ECHO_ATTN_ABLS(4, 2); break;
     case 1: ECHO_ATTN_ABLS(8, 2); break;
@@ -1447,16 +1462,12 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       break;
     }
     case 6: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 2, 32); break;
-    case 9:  // 2 waves x 32 queries per workgroup (production for launches that cannot fill the CUs)
+    case 9:  // 2 waves x 32 queries per workgroup
       if (abl) return ECHO_EINVAL;
       hipLaunchKernelGGL((attn_bf16_kernel<0, 2, 2>), dim3(attn_grid(a, 64)), dim3(128), 0, s, *a, (float*)nullptr, 1);
       break;
     case 7: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 3, 32); break;
     case 10: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(2048, 4, 2); break;  // per-lane epilogue
-    case 11:  // asm-owned software pipeline (production for non-causal launches)
-      if (abl || any_causal(a)) return ECHO_EINVAL;
-      hipLaunchKernelGGL(attn_pl_kernel<0>, grid, dim3(256), 0, s, *a);
-      break;
     case 30:  // one wave per SIMD, 64 queries per wave, two waves per workgroup (measured slower)
       if (abl || any_causal(a)) return ECHO_EINVAL;
       hipLaunchKernelGGL((attn_w64_kernel<0, 2>), grid, dim3(128), 0, s, *a);
@@ -1465,7 +1476,6 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       if (abl || any_causal(a)) return ECHO_EINVAL;
       hipLaunchKernelGGL((attn_w64_kernel<0, 4>), dim3(attn_grid(a, 256)), dim3(256), 0, s, *a);
       break;
-#ifdef ECHO_DIAG
     // ablations of the asm-owned kernels (timing only, results wrong; DESIGN.md §3 lists what each showed):
     // attn_pl_kernel ABL bits 12-18, 8 waves x 32 queries 20-22, attn_w64_kernel 31-33 / 41-43 (16 no tile loop,
     // 1 no loop DMA, 8 no end-of-tile wait)
@@ -1498,13 +1508,13 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       else hipLaunchKernelGGL((attn_pl_kernel<6, 8>), g8, dim3(512), 0, s, *a);
       break;
     }
-#endif
     default: return ECHO_EINVAL;
   }
 #undef ECHO_ATTN_ABLS
 #undef ECHO_ATTN_LAUNCH
   ECHO_LAUNCH_CHECK();
   return 0;
+#endif  // ECHO_DIAG
 }
 
 }  // namespace
@@ -1523,9 +1533,12 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
     // each wave issues twice the DMA; that case takes split-KV chains, echo_attention_split)
     // non-causal launches (every decoder attention) run the asm-owned pipeline (attn_pl_kernel, bitwise
     // equal to attn_bf16_kernel<0, 4, 2>); causal ones (speaker / latent encoders) the compiler-scheduled kernel
+#ifdef ECHO_DIAG
     if (g_attn_pl == 2 && !any_causal(a))
       hipLaunchKernelGGL((attn_w64_kernel<0, 4>), dim3(attn_grid(a, 256)), dim3(256), 0, s, *a);
-    else if (g_attn_pl && !any_causal(a))
+    else
+#endif
+    if (g_attn_pl && !any_causal(a))
       hipLaunchKernelGGL(attn_pl_kernel<0>, dim3(attn_grid(a, 128)), dim3(256), 0, s, *a);
     else
       hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1);
@@ -1582,7 +1595,11 @@ extern "C" int32_t echo_attention_pick_split(const EchoAttnArgs* a) {
 }
 
 extern "C" int echo_attention_set_pipeline(int32_t on) {
-  if (on < 0 || on > 2) return ECHO_EINVAL;
+#ifdef ECHO_DIAG
+  if (on < 0 || on > 2) return ECHO_EINVAL;  // 2: attn_w64_kernel (diagnostics build only)
+#else
+  if (on < 0 || on > 1) return ECHO_EINVAL;
+#endif
   g_attn_pl = on;
   return 0;
 }
@@ -1616,6 +1633,9 @@ extern "C" int echo_attention_variant(const EchoAttnArgs* a, int32_t variant, in
   if (rc) return rc;
   if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
   if ((ablation & 640) && (!stamps || variant > 4)) return ECHO_EINVAL;  // stamps: attn_bf16_kernel variants
+#ifndef ECHO_DIAG
+  if (ablation) return ECHO_EINVAL;  // ablations and stamps: diagnostics build only
+#endif
   if (ablation & 640) {
     if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_attn_stamps), &stamps, sizeof(stamps), 0, hipMemcpyHostToDevice,
                                (hipStream_t)stream) != hipSuccess)

@@ -429,7 +429,12 @@ int echo_cast_from_f32(int32_t dtype, const float* x, void* y, int64_t n, void* 
   return 0;
 }
 
-const char* echo_version(void) { return "echo_hip gfx950 r5 abi6 " __DATE__ " " __TIME__; }
+#ifdef ECHO_DIAG
+#define ECHO_BUILD_KIND "diag "  // diagnostics build: measurement variants and ablations compiled in
+#else
+#define ECHO_BUILD_KIND ""
+#endif
+const char* echo_version(void) { return "echo_hip gfx950 r6 abi6 " ECHO_BUILD_KIND __DATE__ " " __TIME__; }
 
 int32_t echo_abi_version(void) { return ECHO_ABI_VERSION; }
 

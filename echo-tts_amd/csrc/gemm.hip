@@ -2645,6 +2645,83 @@ int launch_sk_cfg(const EchoGemmArgs* a, const Epi& ep, int c, int S, void* ws, 
   }
 }
 
+// The auto plan of a `tile` == 0 launch (host only). echo_gemm_ws launches what it returns and
+// echo_gemm_planned_tile reports it, so the labels bench.py / perf_model.py put on timed launches are the launches
+// production makes. Decisions in order: the small-M family (sk_plan), the large-tile pick (256x256 -> the persistent
+// kernel, or the 2-phase one for a one-round head norm), an unfused head norm (store + echo_head_norm_rope), fp32,
+// the 320-row column split, 320-row tiles, the W13 column split at 1537-2048 rows, the row-tail split.
+enum { RT_SK = 1, RT_TILE, RT_HN_SPLIT, RT_F32, RT_T320_COLSPLIT, RT_T320, RT_W13_COLSPLIT, RT_ROWSPLIT };
+struct Route {
+  int kind = RT_TILE;
+  int t = 0;               // large-tile config (RT_TILE) / the 256x256 kernel of a split
+  int c = 0, S = 1;        // RT_SK: small-M config and K split
+  bool sk_ws = false;      // RT_SK: uses the workspace
+  int c1 = 0;              // RT_*_COLSPLIT: tile columns of the first launch
+  int M1 = 0, tail = 0;    // RT_ROWSPLIT: rows of the 256x256 rounds, the tail's config
+};
+
+Route plan_route(const EchoGemmArgs* a, const void* ws, int64_t ws_bytes) {
+  Route r;
+  int c = 0, S = 1;
+  if (sk_plan(a, ws != nullptr, &c, &S)) {
+    const int64_t need = sk_ws_bytes(a, c, S);
+    if (need == 0 || (ws && (uintptr_t)ws % 16 == 0 && ws_bytes >= need)) {
+      r.kind = RT_SK; r.c = c; r.S = S; r.sk_ws = need > 0;
+      return r;
+    }
+    if (sk_plan(a, false, &c, &S) && sk_ws_bytes(a, c, S) == 0) {  // the best plan without a workspace
+      r.kind = RT_SK; r.c = c; r.S = S;
+      return r;
+    }
+  }
+  const bool headnorm = a->epilogue == ECHO_EPI_HEADNORM;
+  int t = pick_tile(a->M, a->N, a->K, a->batch);
+  // Head norm in at most one tile round (the C2 CFG step's QKVG, M = 1920: 256 tiles): the 2-phase kernel with its
+  // LDS-staged epilogue, 63.3 -> 60.7 us against the persistent kernel's register epilogue, which gains nothing
+  // from persistence in one round (launches replayed from a graph, profiles/r5_sk_1920_sweep.txt; bitwise equal)
+  if (t == 1) {
+    const int64_t tiles = (int64_t)((a->M + 255) / 256) * ((a->N + 255) / 256) * a->batch;
+    const bool one_round_hn = headnorm && tiles <= cu_count_cached();
+    t = (a->dtype == ECHO_BF16 && ps_ok(a, ek_of(a)) && !g_gemm_no_ps && !one_round_hn) ? 16 : 13;
+  }
+  r.t = t;
+  // fused on the persistent kernel (t 16, via ps_ok) or the 2-phase one (t 13)
+  const bool hn_fused = a->dtype == ECHO_BF16 && ((t == 13 && a->N % 128 == 0) || (t == 16 && ps_ok(a, EK_HEADNORM)));
+  if (headnorm && !hn_fused) { r.kind = RT_HN_SPLIT; return r; }
+  if (a->dtype == ECHO_F32) { r.kind = RT_F32; return r; }
+  const int cus = cu_count_cached();
+  if (g_gemm_t320 == 0 && !g_gemm_no_colsplit && a->batch == 1 && !headnorm && t320_ok(a)) {
+    const int c1 = t320_col_split(a, cus);
+    if (c1 > 0) { r.kind = RT_T320_COLSPLIT; r.c1 = c1; return r; }
+  }
+  if (g_gemm_t320 != 1 && t320_ok(a)) {
+    const int n320 = (a->M / 320) * (a->N / 256);
+    if (g_gemm_t320 == 2 ? n320 >= cus : t320_pays(a, cus)) { r.kind = RT_T320; return r; }
+  }
+  // SwiGLU at 1537..2048 rows (W13 of the B = 1 CFG step, M = 1920: 8 x 46 = 368 tiles, two rounds of the
+  // persistent 256x256 kernel): the first ⌊0.94 CUs / row tiles⌋ tile columns there (one round) and the rest on
+  // the small-M 128x256 8-wave config (one round of half tiles) — 98.8 -> 88.2 us (profiles/r5_colsplit.txt).
+  // Same K order per element: bitwise equal.
+  if (!g_gemm_no_colsplit && !g_gemm_no_sk && a->batch == 1 && t == 16 && ek_of(a) == EK_SWIGLU && a->N % 256 == 0) {
+    const int tm = (a->M + 255) / 256, tn = a->N / 256;
+    const int c1 = (int)(0.94 * cus) / tm;
+    if ((tm == 7 || tm == 8) && tm * tn > cus && tm * tn < 2 * cus && c1 > 0 && c1 < tn) {
+      EchoGemmArgs rest = *a;
+      rest.N = a->N - c1 * 256;
+      rest.W = (const bf16_t*)a->W + (int64_t)c1 * 256 * a->ldw;
+      rest.C = (bf16_t*)a->C + c1 * 128;
+      rest.tile = 100 + 10 * 13 + 1;
+      if (sk_ok(&rest)) { r.kind = RT_W13_COLSPLIT; r.c1 = c1; return r; }
+    }
+  }
+  if ((t == 13 || t == 16) && a->batch == 1 && !headnorm && !g_gemm_no_rowsplit) {
+    int tail = 0;
+    const int M1 = split_rows(a->M, a->N, &tail);
+    if (M1 > 0) { r.kind = RT_ROWSPLIT; r.M1 = M1; r.tail = tail; return r; }
+  }
+  return r;
+}
+
 extern int g_adaln_blocks;  // elementwise.hip
 
 extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
@@ -2690,18 +2767,21 @@ extern "C" int64_t echo_gemm_ws_bytes(const EchoGemmArgs* a) {
 }
 
 // the launch echo_gemm_ws would make for these arguments with a workspace of ws_bytes (host only; perf_model.py
-// labels its timed launches with it): 100 + 10 c + S for the small-M config c split S ways, else the large-tile
-// pick (13 = the 256x256 / 320x256 family)
+// labels its timed launches with it): plan_route's decision as a code (echo_hip.h)
 extern "C" int32_t echo_gemm_planned_tile(const EchoGemmArgs* a, int64_t ws_bytes) {
   if (!a || a->M <= 0 || a->N <= 0 || a->K <= 0 || a->K % BK) return 0;
   if (a->tile != 0) return a->tile;
-  int c = 0, S = 1;
-  if (sk_plan(a, ws_bytes > 0, &c, &S)) {
-    const int64_t need = sk_ws_bytes(a, c, S);
-    if (need == 0 || ws_bytes >= need) return 100 + 10 * c + S;
-    if (sk_plan(a, false, &c, &S) && sk_ws_bytes(a, c, S) == 0) return 100 + 10 * c + S;
+  const Route r = plan_route(a, ws_bytes > 0 ? (const void*)(uintptr_t)256 : nullptr, ws_bytes);
+  switch (r.kind) {
+    case RT_SK: return 100 + 10 * r.c + r.S;
+    case RT_T320: return 20;
+    case RT_T320_COLSPLIT: return 201;
+    case RT_W13_COLSPLIT: return 202;
+    case RT_ROWSPLIT: return 203;
+    case RT_HN_SPLIT: return 204;
+    case RT_F32: return 205;
+    default: return r.t;
   }
-  return echo_gemm_pick_tile(a->M, a->N, a->K, a->batch);
 }
 
 extern "C" int echo_gemm(const EchoGemmArgs* a, void* stream) { return echo_gemm_ws(a, nullptr, 0, stream); }
@@ -2773,7 +2853,7 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
     return echo_adaln_modulate(a->dtype, a->C, a->mod_out, a->M, a->N, a->mod_shift, a->mod_scale1, 0, 0,
                                a->mod_eps, stream);
   }
-  // small-M family (gemm_bf16_sk_kernel): forced (`tile` 1CS) or the auto pick of under-filled launches
+  // small-M family (gemm_bf16_sk_kernel) forced by `tile` 1CS
   if (sk_tile(a->tile)) {
     const int c = (a->tile - 100) / 10, S = a->tile % 10;
     if (c < 1 || c > kNumSk || S < 1 || !sk_ok(a) || a->K / BK < S) return ECHO_EINVAL;
@@ -2781,35 +2861,8 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
     if (need > 0 && (!ws || (uintptr_t)ws % 16 || ws_bytes < need)) return ECHO_EINVAL;
     return launch_sk_cfg(a, ep, c, S, ws, (hipStream_t)stream);
   }
-  if (a->tile == 0) {
-    int c = 0, S = 1;
-    if (sk_plan(a, ws != nullptr, &c, &S)) {
-      const int64_t need = sk_ws_bytes(a, c, S);
-      if (need == 0 || (ws && (uintptr_t)ws % 16 == 0 && ws_bytes >= need))
-        return launch_sk_cfg(a, ep, c, S, ws, (hipStream_t)stream);
-      if (sk_plan(a, false, &c, &S) && sk_ws_bytes(a, c, S) == 0)  // the best plan without a workspace
-        return launch_sk_cfg(a, ep, c, S, nullptr, (hipStream_t)stream);
-    }
-  }
-  if (a->tile == 18) ep.gm = g_gemm_gm;
-  if (a->tile == 15) ep.epi = 99;  // diagnostic: no epilogue
-  int t = a->tile > 0 ? a->tile : pick_tile(a->M, a->N, a->K, a->batch);
-  // 256x256 tiles run the persistent 2-phase kernel where its register epilogue applies, else the
-  // 2-phase ping-pong (all bitwise-identical results)
-  // Head norm in at most one tile round (the C2 CFG step's QKVG, M = 1920: 256 tiles): the 2-phase kernel with its
-  // LDS-staged epilogue, 63.3 -> 60.7 us against the persistent kernel's register epilogue, which gains nothing
-  // from persistence in one round (launches replayed from a graph, profiles/r5_sk_1920_sweep.txt; bitwise equal)
-  if (a->tile == 0 && t == 1) {
-    const int64_t tiles = (int64_t)((a->M + 255) / 256) * ((a->N + 255) / 256) * a->batch;
-    const bool one_round_hn = headnorm && tiles <= cu_count_cached();
-    t = (a->dtype == ECHO_BF16 && ps_ok(a, ek_of(a)) && !g_gemm_no_ps && !one_round_hn) ? 16 : 13;
-  }
-  // fused on the persistent kernel (t 16/17/18, N % 256 == 0, via ps_ok) or the 2-phase one (t 13)
-  const bool hn_fused = a->dtype == ECHO_BF16 && ((t == 13 && a->N % 128 == 0) ||
-                                                   ((t == 16 || t == 18) && ps_ok(a, EK_HEADNORM)) ||
-                                                   ((t >= 20 && t <= 23) && t320_ok(a)));
-  if (headnorm && !hn_fused) {
-    // not fused for this shape / dtype: plain store, then the standalone kernel (same results)
+  // head norm not fused for this shape / dtype: plain store, then the standalone kernel (same results)
+  auto hn_split = [&]() -> int {
     EchoGemmArgs b = *a;
     b.epilogue = ECHO_EPI_STORE;
     const int rc = echo_gemm(&b, stream);
@@ -2817,81 +2870,52 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
     return echo_head_norm_rope(a->dtype, a->C, a->ldc, a->M, a->hn_heads, a->hn_nblk, 0,
                                (int64_t)a->hn_heads * 128, a->hn_w, a->hn_w_stride, a->hn_rope, a->hn_rope_heads,
                                a->hn_seq_len, a->hn_pos0, a->hn_pos_mult, a->hn_eps, stream);
-  }
-  if (a->dtype == ECHO_F32 && f32_mfma_ok(a)) {
-    dim3 grid((a->N + QN - 1) / QN, (a->M + QM - 1) / QM, a->batch);
-    hipLaunchKernelGGL(gemm_f32_mfma_kernel, grid, dim3(256), 0, s, (const float*)a->A, a->lda, a->stride_a,
-                       (const float*)a->W, a->ldw, a->stride_w, a->C, a->ldc, a->stride_c, a->M, a->N,
-                       a->K, ep);
+  };
+  auto run_f32 = [&]() -> int {
+    if (f32_mfma_ok(a)) {
+      dim3 grid((a->N + QN - 1) / QN, (a->M + QM - 1) / QM, a->batch);
+      hipLaunchKernelGGL(gemm_f32_mfma_kernel, grid, dim3(256), 0, s, (const float*)a->A, a->lda, a->stride_a,
+                         (const float*)a->W, a->ldw, a->stride_w, a->C, a->ldc, a->stride_c, a->M, a->N,
+                         a->K, ep);
+    } else {
+      dim3 grid((a->N + FT - 1) / FT, (a->M + FT - 1) / FT, a->batch);
+      hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, s, (const float*)a->A, a->lda, a->stride_a,
+                         (const float*)a->W, a->ldw, a->stride_w, a->C, a->ldc, a->stride_c, a->M, a->N,
+                         a->K, ep);
+    }
     ECHO_LAUNCH_CHECK();
     return 0;
-  }
-  if (a->dtype == ECHO_F32) {
-    dim3 grid((a->N + FT - 1) / FT, (a->M + FT - 1) / FT, a->batch);
-    hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, s, (const float*)a->A, a->lda, a->stride_a,
-                       (const float*)a->W, a->ldw, a->stride_w, a->C, a->ldc, a->stride_c, a->M, a->N,
-                       a->K, ep);
-    ECHO_LAUNCH_CHECK();
-    return 0;
-  }
-  if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
-  if (((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C) & 15) return ECHO_EALIGN;
-  // gated residual / SwiGLU / head norm at M = 320 k: 320-row tiles when they need fewer 1.2x tile-rounds than
-  // 256x256 tiles (t320_pays); tile 20 forces them (bitwise equal either way)
-  if (a->tile == 20) return t320_ok(a) ? launch_t320(a, ep, s) : ECHO_EINVAL;
-  if (a->tile == 21) return t320_ok(a) ? launch_t320_sp<1, 0>(a, ep, s) : ECHO_EINVAL;  // 4 / 5 DMA split (A/B)
-  if (a->tile == 22) return t320_ok(a) ? launch_t320_sp<0, 0>(a, ep, s) : ECHO_EINVAL;  // one tile per workgroup
-  if (a->tile == 23) return t320_ok(a) ? launch_t320_sp<0, 1>(a, ep, s) : ECHO_EINVAL;  // persistent
-  if (a->tile == 0 && g_gemm_t320 == 0 && !g_gemm_no_colsplit && a->batch == 1 && !headnorm && t320_ok(a)) {
-    const int c1 = t320_col_split(a, cu_count_cached());
-    if (c1 > 0) {
-      // two launches on the same stream: tile columns [0, c1) on 320-row tiles, the rest by the auto pick
-      const int n1 = c1 * 256;
-      EchoGemmArgs h = *a, r = *a;
-      h.N = n1;
-      h.tile = 20;
-      r.N = a->N - n1;
-      r.W = (const bf16_t*)a->W + (int64_t)n1 * a->ldw;
-      r.C = (bf16_t*)a->C + (a->epilogue == ECHO_EPI_SWIGLU ? n1 / 2 : n1);
-      if (a->aux) r.aux = (const bf16_t*)a->aux + n1;
-      if (a->gate) r.gate = (const bf16_t*)a->gate + n1;
-      if (a->bias) r.bias = (const bf16_t*)a->bias + n1;
-      const int rc = echo_gemm(&h, stream);
-      return rc ? rc : echo_gemm(&r, stream);
-    }
-  }
-  if (a->tile == 0 && g_gemm_t320 != 1 && t320_ok(a)) {
-    const int n320 = (a->M / 320) * (a->N / 256), cus = cu_count_cached();
-    if (g_gemm_t320 == 2 ? n320 >= cus : t320_pays(a, cus)) return launch_t320(a, ep, s);
-  }
-  // SwiGLU at 1537..2048 rows (W13 of the B = 1 CFG step, M = 1920: 8 x 46 = 368 tiles, two rounds of the
-  // persistent 256x256 kernel): the first ⌊0.94 CUs / row tiles⌋ tile columns there (one round) and the rest on
-  // the small-M 128x256 8-wave config (one round of half tiles) — 98.8 -> 88.2 us (profiles/r5_colsplit.txt).
-  // Same K order per element: bitwise equal.
-  if (a->tile == 0 && !g_gemm_no_colsplit && !g_gemm_no_sk && a->batch == 1 && t == 16 && ek_of(a) == EK_SWIGLU &&
-      a->N % 256 == 0) {
-    const int tm = (a->M + 255) / 256, tn = a->N / 256, cus = cu_count_cached();
-    const int c1 = (int)(0.94 * cus) / tm;
-    if ((tm == 7 || tm == 8) && tm * tn > cus && tm * tn < 2 * cus && c1 > 0 && c1 < tn) {
-      const int n1 = c1 * 256;
-      EchoGemmArgs h = *a, r = *a;
-      h.N = n1;
-      h.tile = 16;
-      r.N = a->N - n1;
-      r.W = (const bf16_t*)a->W + (int64_t)n1 * a->ldw;
-      r.C = (bf16_t*)a->C + n1 / 2;
-      r.tile = 100 + 10 * 13 + 1;
-      if (sk_ok(&r)) {
-        const int rc = echo_gemm(&h, stream);
-        return rc ? rc : echo_gemm(&r, stream);
-      }
-    }
-  }
-  int tail_cfg = 0;
-  const int M1 = (a->tile == 0 && (t == 13 || t == 16) && a->batch == 1 && !headnorm && !g_gemm_no_rowsplit)
-                     ? split_rows(a->M, a->N, &tail_cfg) : 0;
-  if (M1 > 0) {
-    // two launches on the same stream: full rounds of the 256x256 kernel, then the row tail
+  };
+  // two launches on the same stream: tile columns [0, c1) on 320-row tiles (whole rounds), the rest by the auto pick
+  auto t320_colsplit = [&](int c1) -> int {
+    const int n1 = c1 * 256;
+    EchoGemmArgs h = *a, r = *a;
+    h.N = n1;
+    h.tile = 20;
+    r.N = a->N - n1;
+    r.W = (const bf16_t*)a->W + (int64_t)n1 * a->ldw;
+    r.C = (bf16_t*)a->C + (a->epilogue == ECHO_EPI_SWIGLU ? n1 / 2 : n1);
+    if (a->aux) r.aux = (const bf16_t*)a->aux + n1;
+    if (a->gate) r.gate = (const bf16_t*)a->gate + n1;
+    if (a->bias) r.bias = (const bf16_t*)a->bias + n1;
+    const int rc = echo_gemm(&h, stream);
+    return rc ? rc : echo_gemm(&r, stream);
+  };
+  // W13 at 1537..2048 rows: tile columns [0, c1) on the persistent 256x256 kernel, the rest on small-M config 13
+  auto w13_colsplit = [&](int c1) -> int {
+    const int n1 = c1 * 256;
+    EchoGemmArgs h = *a, r = *a;
+    h.N = n1;
+    h.tile = 16;
+    r.N = a->N - n1;
+    r.W = (const bf16_t*)a->W + (int64_t)n1 * a->ldw;
+    r.C = (bf16_t*)a->C + n1 / 2;
+    r.tile = 100 + 10 * 13 + 1;
+    const int rc = echo_gemm(&h, stream);
+    return rc ? rc : echo_gemm(&r, stream);
+  };
+  // two launches on the same stream: full rounds of the 256x256 kernel, then the row tail
+  auto rowsplit = [&](int M1, int tail_cfg, int t) -> int {
     EchoGemmArgs h = *a, r = *a;
     h.M = M1;
     h.tile = t;
@@ -2903,23 +2927,58 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
     if (a->aux) r.aux = (const bf16_t*)a->aux + (int64_t)M1 * a->ld_aux;
     const int rc = echo_gemm(&h, stream);
     return rc ? rc : echo_gemm(&r, stream);
+  };
+  auto run_tile = [&](int t) -> int {
+    switch (t) {
+      case 1: return launch_bf16<256, 256, 2, 4>(a, ep, s);
+      case 2: return launch_bf16<256, 128, 4, 2>(a, ep, s);
+      case 3: return launch_bf16<128, 128, 2, 2>(a, ep, s);
+      case 4: return launch_bf16<128, 64, 2, 2>(a, ep, s);
+      case 5: return launch_bf16<64, 64, 2, 2>(a, ep, s);
+      case 6: return launch_pp<0>(a, ep, s);
+      case 7: return launch_pp<1>(a, ep, s);
+      case 8: return launch_pp<2>(a, ep, s);
+      case 9: return launch_pp<3>(a, ep, s);
+      case 10: return launch_pp<4>(a, ep, s);
+      case 11: return launch_pp<8>(a, ep, s);
+      case 12: return launch_pp<11>(a, ep, s);
+      case 13: case 15: return launch_pp2(a, ep, s);
+      case 16: return ps_ok(a, ek_of(a)) ? launch_ps(a, ep, s) : launch_pp2(a, ep, s);
+      case 18: return ps_ok(a, ek_of(a)) ? launch_ps(a, ep, s) : ECHO_EINVAL;  // group-M override (diag key 1)
+      default: return ECHO_EINVAL;
+    }
+  };
+  const bool misaligned = ((uintptr_t)a->A | (uintptr_t)a->W | (uintptr_t)a->C) & 15;
+  if (a->tile == 0) {  // the auto plan (plan_route; echo_gemm_planned_tile reports the same decision)
+    const Route r = plan_route(a, ws, ws_bytes);
+    if (r.kind == RT_SK) return launch_sk_cfg(a, ep, r.c, r.S, r.sk_ws ? ws : nullptr, s);
+    if (r.kind == RT_HN_SPLIT) return hn_split();
+    if (r.kind == RT_F32) return run_f32();
+    if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
+    if (misaligned) return ECHO_EALIGN;
+    switch (r.kind) {
+      case RT_T320_COLSPLIT: return t320_colsplit(r.c1);
+      case RT_T320: return launch_t320(a, ep, s);
+      case RT_W13_COLSPLIT: return w13_colsplit(r.c1);
+      case RT_ROWSPLIT: return rowsplit(r.M1, r.tail, r.t);
+      default: return run_tile(r.t);
+    }
   }
-  switch (t) {
-    case 1: return launch_bf16<256, 256, 2, 4>(a, ep, s);
-    case 2: return launch_bf16<256, 128, 4, 2>(a, ep, s);
-    case 3: return launch_bf16<128, 128, 2, 2>(a, ep, s);
-    case 4: return launch_bf16<128, 64, 2, 2>(a, ep, s);
-    case 5: return launch_bf16<64, 64, 2, 2>(a, ep, s);
-    case 6: return launch_pp<0>(a, ep, s);
-    case 7: return launch_pp<1>(a, ep, s);
-    case 8: return launch_pp<2>(a, ep, s);
-    case 9: return launch_pp<3>(a, ep, s);
-    case 10: return launch_pp<4>(a, ep, s);
-    case 11: return launch_pp<8>(a, ep, s);
-    case 12: return launch_pp<11>(a, ep, s);
-    case 13: case 15: return launch_pp2(a, ep, s);
-    case 16: return ps_ok(a, ek_of(a)) ? launch_ps(a, ep, s) : launch_pp2(a, ep, s);
-    case 18: return ps_ok(a, ek_of(a)) ? launch_ps(a, ep, s) : ECHO_EINVAL;  // group-M override (diag key 1)
-    default: return ECHO_EINVAL;
-  }
+  // forced tile (tests, tools/bench_gemm.py)
+  if (a->tile == 18) ep.gm = g_gemm_gm;
+  if (a->tile == 15) ep.epi = 99;  // diagnostic: no epilogue
+  const int t = a->tile;
+  // fused on the persistent kernel (t 16/18, N % 256 == 0, via ps_ok), the 2-phase one (t 13) or 320-row tiles
+  const bool hn_fused = a->dtype == ECHO_BF16 && ((t == 13 && a->N % 128 == 0) ||
+                                                   ((t == 16 || t == 18) && ps_ok(a, EK_HEADNORM)) ||
+                                                   ((t >= 20 && t <= 23) && t320_ok(a)));
+  if (headnorm && !hn_fused) return hn_split();
+  if (a->dtype == ECHO_F32) return run_f32();
+  if (a->dtype != ECHO_BF16) return ECHO_EDTYPE;
+  if (misaligned) return ECHO_EALIGN;
+  if (t == 20) return t320_ok(a) ? launch_t320(a, ep, s) : ECHO_EINVAL;  // 320-row tiles (auto DMA split)
+  if (t == 21) return t320_ok(a) ? launch_t320_sp<1, 0>(a, ep, s) : ECHO_EINVAL;  // 4 / 5 DMA split (A/B)
+  if (t == 22) return t320_ok(a) ? launch_t320_sp<0, 0>(a, ep, s) : ECHO_EINVAL;  // one tile per workgroup
+  if (t == 23) return t320_ok(a) ? launch_t320_sp<0, 1>(a, ep, s) : ECHO_EINVAL;  // persistent
+  return run_tile(t);
 }

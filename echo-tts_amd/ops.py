@@ -148,7 +148,16 @@ def attention(q: Tensor, segments: Sequence[Segment], out: Optional[Tensor] = No
 # Process-global library switches that change which kernels (and so which summation orders) a launch runs.
 # Their current values are kept here so that context managers restore what they replaced (nested use) and a
 # captured plan can be keyed on them (engine.plan_key via current_split_state()).
-_KNOBS = {"attention_split": -1, "gemm_no_splitk": 0, "attention_pipeline": 1}
+# gemm_no_splitk starts from what ECHO_GEMM_DIAG set at library load (key 11; _lib.DIAG_APPLIED), so the mirror
+# and the plan key never disagree with the library.
+_KNOBS = {"attention_split": -1, "gemm_no_splitk": None, "attention_pipeline": 1}
+
+
+def _knob_value(name: str) -> int:
+    if _KNOBS[name] is None:  # seeded once the library is loaded
+        lib()
+        _KNOBS[name] = int(L.DIAG_APPLIED.get(11, 0))
+    return _KNOBS[name]
 
 
 def _set_knob(name: str, value: int) -> None:
@@ -159,13 +168,13 @@ def _set_knob(name: str, value: int) -> None:
     else:
         rc = lib().echo_attention_set_pipeline(int(value))
     if rc:
-        raise RuntimeError(f"{name}({value}) refused by libecho_hip: {rc}")
+        raise RuntimeError(f"{name}({value}) refused by libecho_hip: {L.ERRORS.get(rc, rc)}")
     _KNOBS[name] = int(value)
 
 
 @contextlib.contextmanager
 def _knob(name: str, value: int):
-    prev = _KNOBS[name]
+    prev = _knob_value(name)
     _set_knob(name, value)
     try:
         yield
@@ -189,7 +198,8 @@ def gemm_no_splitk():
 def attention_pipeline(mode):
     """The kernel of non-causal bf16 attention launches inside the block (A/B tests and measurements):
     1 / True = the asm-owned pipelined kernel (attn_pl_kernel, default), 0 / False = the compiler-scheduled
-    kernel, 2 = one wave per SIMD with 64 queries per wave (attn_w64_kernel). All bitwise equal."""
+    kernel, 2 = one wave per SIMD with 64 queries per wave (attn_w64_kernel; diagnostics build only, the product
+    library refuses it). All bitwise equal."""
     return _knob("attention_pipeline", int(mode))
 
 
@@ -226,7 +236,7 @@ def current_split_state() -> Tuple:
     """Everything process-global that decides the kernels a captured plan holds: the policy rows and the
     split / kernel-choice switches above. Part of a plan's identity (engine.plan_key), so a graph captured
     under one state is never replayed under another."""
-    return (_POLICY, tuple(sorted(_KNOBS.items())))
+    return (_POLICY, tuple(sorted((k, _knob_value(k)) for k in _KNOBS)))
 
 
 def attention_variant(q: Tensor, segments: Sequence[Segment], out: Tensor, gate: Optional[Tensor] = None,

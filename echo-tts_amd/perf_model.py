@@ -75,9 +75,10 @@ def blockwise_flops(cfg: EchoConfig, block_sizes: Sequence[int], steps_cfg: int,
     return out
 
 
-def planned_tile(a, w, out, epilogue: int, aux=None) -> int:
+def planned_tile(a, w, out, epilogue: int, aux=None, head_norm=None) -> int:
     """The launch the library plans for this GEMM (echo_gemm_planned_tile with the workspace the torch op would
-    allocate): 100 + 10 c + S for the small-M config c split S ways, else the large-tile pick."""
+    allocate; codes in include/echo_hip.h): 100 + 10 c + S for the small-M config c split S ways, 201-203 the
+    column / row splits, else the large-tile kernel."""
     from . import _lib
     lib = _lib.load()
     g = _lib.GemmArgs()
@@ -90,6 +91,13 @@ def planned_tile(a, w, out, epilogue: int, aux=None) -> int:
     g.epilogue = epilogue
     if aux is not None:
         g.aux, g.ld_aux = aux.data_ptr(), aux.stride(-2)
+    if head_norm is not None:  # ECHO_EPI_HEADNORM: the plan depends on the head layout
+        g.epilogue = _lib.EPI_HEADNORM
+        g.hn_w, g.hn_w_stride, g.hn_heads, g.hn_nblk = head_norm.w.data_ptr(), head_norm.w_stride, head_norm.heads, \
+            head_norm.nblk
+        g.hn_rope_heads, g.hn_seq_len = head_norm.rope_heads, head_norm.seq_len
+        if head_norm.rope is not None:
+            g.hn_rope = head_norm.rope.data_ptr()
     import ctypes
     return int(lib.echo_gemm_planned_tile(ctypes.byref(g), lib.echo_gemm_ws_bytes(ctypes.byref(g))))
 
@@ -128,7 +136,8 @@ class GemmTimer:
             osz = 4 if kw.get("epilogue", 0) == _lib.EPI_F32OUT else 2
             byts = 2 * (M * K * (a.shape[0] if a.dim() == 3 else 1) + N * K * (w.shape[0] if w.dim() == 3 else 1)) \
                 + osz * M * nout * batch + (2 * M * nout * batch if kw.get("aux") is not None else 0)
-            lab = planned_tile(a, w, out, kw.get("epilogue", 0), kw.get("aux")) if batch == 1 and a.dim() == 2 else tile
+            lab = (planned_tile(a, w, out, kw.get("epilogue", 0), kw.get("aux"), kw.get("head_norm"))
+                   if batch == 1 and a.dim() == 2 else tile)
             timer.records.append((e0, e1, 2.0 * M * N * K * batch, lab, (M, N, K, batch), byts))
             return r
 

@@ -102,8 +102,12 @@ int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch);
  * split launch sums K in S contiguous partial sums (fp32; the unsplit kernels all share one K order).
  * The workspace is only touched by the launched kernels (stream-ordered, capturable). */
 int64_t echo_gemm_ws_bytes(const EchoGemmArgs* args);
-/* Host-only query: the launch echo_gemm_ws(args, ws, ws_bytes, .) would make — 100 + 10 c + S for the small-M
- * config c with K split S ways, otherwise echo_gemm_pick_tile's large-tile pick (bench.py's per-launch labels). */
+/* Host-only query: the launch echo_gemm_ws(args, ws, ws_bytes, .) would make (the same host routine decides both;
+ * bench.py's per-launch labels): 100 + 10 c + S = the small-M config c with K split S ways; 2..5 the smaller tile
+ * configs; 13 the 2-phase 256x256 kernel; 16 the persistent 256x256 kernel; 20 320-row tiles; 201 the 320-row column
+ * split (whole rounds of 320-row tile columns, the rest by the auto pick); 202 the W13 column split at 1537-2048 rows
+ * (persistent 256x256 kernel + small-M config 13); 203 the row-tail split (256x256 rounds + a smaller-tile tail);
+ * 204 store + echo_head_norm_rope (head norm not fused for the shape); 205 fp32; a forced `tile` is returned as is. */
 int32_t echo_gemm_planned_tile(const EchoGemmArgs* args, int64_t ws_bytes);
 int echo_gemm_ws(const EchoGemmArgs* args, void* ws, int64_t ws_bytes, void* stream);
 
@@ -122,8 +126,9 @@ int echo_set_policy_rows(int32_t num, int32_t den);
  * smaller tile (default 128); key 6: cap on the persistent kernel's workgroup count (0 = one per CU);
  * key 7: 320x256 tiles for the gated residual / SwiGLU / head norm (0 = when they need fewer 1.2x
  * tile-rounds than 256x256 tiles, 1 = never, 2 = whenever they fill at least one round); key 8: 1 = no
- * column split of auto-picked 320-row launches (W13: 320-row tiles on whole rounds of tile columns, the
- * rest on the persistent 256x256 kernel); key 9: block cap of the wave-per-row AdaLN kernel (0 = 8192);
+ * column split of auto-picked launches: neither the 320-row one (W13 at M = 320 k: 320-row tiles on whole rounds
+ * of tile columns, the rest on the persistent 256x256 kernel) nor the W13 one at 1537-2048 rows (one round of the
+ * persistent 256x256 kernel, the rest on small-M config 13); key 9: block cap of the wave-per-row AdaLN kernel (0 = 8192);
  * (`tile` 22 / 23 force one 320-row tile per workgroup / the persistent 320-row kernel for any epilogue;
  * A/B timing, all bitwise-equal; key 10 is retired.)
  * key 11: 1 = never split K in echo_gemm_ws (the B = 1 runs that tests compare bitwise with B = 16 rows);
@@ -176,7 +181,8 @@ int32_t echo_attention_pick_split(const EchoAttnArgs* args);
 int echo_attention_set_split(int32_t nsplit);
 /* Diagnostics: 1 (default) = non-causal bf16 launches run the asm-owned software-pipelined kernel
  * (attn_pl_kernel, bitwise equal to the compiler-scheduled one), 0 = the compiler-scheduled kernel for
- * every launch (A/B measurements). */
+ * every launch (A/B measurements); 2 = attn_w64_kernel (one wave per SIMD, 64 queries per wave; measured
+ * slower) in the diagnostics build (ECHO_DIAG=1) only — the product library refuses 2 with ECHO_EINVAL. */
 int echo_attention_set_pipeline(int32_t on);
 
 /* Diagnostics only (tools/bench_attn.py, tools/attn_timeline.py; never on the sampling path):
@@ -185,6 +191,8 @@ int echo_attention_set_pipeline(int32_t on);
  * records per-workgroup s_memrealtime stamps into `stamps` (device, [workgroups][6] uint64:
  * entry, prologue landed, tile loop done, exit, tiles, XCD); bit 512 (with 128) additionally
  * records per-tile phase cycles of workgroup 0 after that area ([4 waves][64][6]).
+ * The product library accepts variant 0 and 11 (attn_pl_kernel) with ablation 0 and refuses everything
+ * else with ECHO_EINVAL; the diagnostics build (ECHO_DIAG=1) has every variant and ablation.
  * Variants/bits: csrc/attention.hip. */
 int echo_attention_variant(const EchoAttnArgs* args, int32_t variant, int32_t ablation, uint64_t* stamps,
                            void* stream);

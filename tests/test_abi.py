@@ -244,9 +244,13 @@ def test_gemm_small_m_plan_host_policy(lib):
     planned = lambda M, N, K, wsb, epi=L.EPI_RESID: lib.echo_gemm_planned_tile(C.byref(args(M, N, K, epi)), wsb)  # noqa: E731
     assert planned(160, 2048, 5888, 4 * 160 * 2048 * 4) == 154
     assert planned(480, 2048, 2048, 0) == 181           # config 8 unsplit, direct epilogue
-    assert planned(30720, 2048, 5888, 0) == lib.echo_gemm_pick_tile(30720, 2048, 5888, 1)
+    assert planned(30720, 2048, 5888, 0) == 20          # C3 W2: 320-row tiles (whole rounds)
+    assert planned(1920, 11776, 2048, 0, L.EPI_SWIGLU) == 202  # C2 CFG W13: persistent 256x256 + small-M column split
+    assert planned(30720, 11776, 2048, 0, L.EPI_SWIGLU) == 201  # C3 W13: 320-row column split
     assert lib.echo_attention_set_pipeline(3) != 0 and lib.echo_attention_set_pipeline(-1) != 0
     assert lib.echo_attention_set_pipeline(0) == 0 and lib.echo_attention_set_pipeline(1) == 0
+    if " diag " not in lib.echo_version().decode():  # attn_w64_kernel: diagnostics build only
+        assert lib.echo_attention_set_pipeline(2) == -1  # ECHO_EINVAL
 
 
 def test_asm_owned_attention_registers_untouched():
@@ -254,8 +258,11 @@ def test_asm_owned_attention_registers_untouched():
     out of the owned VGPRs, nothing but this check keeps it out of the owned AGPRs), and those kernels do not
     spill (tools/check_owned_regs.py on the gfx950 assembly of the diagnostics build, ECHO_DIAG=1: the product
     kernels plus every timing-ablation instantiation, so the diagnostics build is compiled here too)."""
+    import shutil
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not (os.environ.get("HIPCC") or os.path.exists("/opt/rocm/bin/hipcc") or shutil.which("hipcc")):
+        pytest.skip("hipcc not installed")
     r = subprocess.run([sys.executable, os.path.join(repo, "tools", "check_owned_regs.py"), "--compile-to",
                         "/tmp/echo_attention_check_diag.s"],
                        capture_output=True, text=True, timeout=900, env={**os.environ, "ECHO_DIAG": "1"})

@@ -22,8 +22,18 @@ CSRC = os.path.join(REPO, "echo-tts_amd", "csrc")
 KERNELS = {"attn_pl_kernel": (96, None), "attn_w64_kernel": (128, 224)}
 
 
+def hipcc():
+    """The hipcc echo-tts_amd/build.py uses ($HIPCC, /opt/rocm/bin/hipcc, or hipcc on PATH)."""
+    sys.path.insert(0, os.path.join(REPO, "echo-tts_amd"))
+    try:
+        from build import _hipcc
+    finally:
+        sys.path.pop(0)
+    return _hipcc()
+
+
 def compile_asm(out):
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
            f"-I{os.path.join(REPO, 'include')}", "--cuda-device-only",
            *(["-DECHO_DIAG"] if os.environ.get("ECHO_DIAG") == "1" else []), "-S", os.path.join(CSRC, "attention.hip"),
            "-o", out]
