@@ -54,7 +54,7 @@ class Arena:
         flat = self.region[: self.n // es * es].view(dtype)
         if strides is None:
             strides = torch.empty(shape).stride()
-        t = flat.as_strided(shape, strides, offset)
+        t = flat.as_strided(shape, strides, flat.storage_offset() + offset)  # storage offsets are absolute
         m = torch.zeros(flat.numel(), dtype=torch.bool, device=DEV)
         m.as_strided(shape, strides, offset).fill_(True)
         self.own[: m.numel() * es] |= m.repeat_interleave(es)
