@@ -2936,13 +2936,17 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
       case 4: return launch_bf16<128, 64, 2, 2>(a, ep, s);
       case 5: return launch_bf16<64, 64, 2, 2>(a, ep, s);
       case 6: return launch_pp<0>(a, ep, s);
+#ifdef ECHO_DIAG
+      // timing ablations of the 4-phase kernel (results wrong): diagnostics build only
       case 7: return launch_pp<1>(a, ep, s);
       case 8: return launch_pp<2>(a, ep, s);
       case 9: return launch_pp<3>(a, ep, s);
       case 10: return launch_pp<4>(a, ep, s);
       case 11: return launch_pp<8>(a, ep, s);
       case 12: return launch_pp<11>(a, ep, s);
-      case 13: case 15: return launch_pp2(a, ep, s);
+      case 15:  // no epilogue (ep.epi = 99 above)
+#endif
+      case 13: return launch_pp2(a, ep, s);
       case 16: return ps_ok(a, ek_of(a)) ? launch_ps(a, ep, s) : launch_pp2(a, ep, s);
       case 18: return ps_ok(a, ek_of(a)) ? launch_ps(a, ep, s) : ECHO_EINVAL;  // group-M override (diag key 1)
       default: return ECHO_EINVAL;
@@ -2966,7 +2970,9 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
   }
   // forced tile (tests, tools/bench_gemm.py)
   if (a->tile == 18) ep.gm = g_gemm_gm;
-  if (a->tile == 15) ep.epi = 99;  // diagnostic: no epilogue
+#ifdef ECHO_DIAG
+  if (a->tile == 15) ep.epi = 99;  // diagnostic: no epilogue (diagnostics build only)
+#endif
   const int t = a->tile;
   // fused on the persistent kernel (t 16/18, N % 256 == 0, via ps_ok), the 2-phase one (t 13) or 320-row tiles
   const bool hn_fused = a->dtype == ECHO_BF16 && ((t == 13 && a->N % 128 == 0) ||

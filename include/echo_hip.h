@@ -134,7 +134,8 @@ int echo_set_policy_rows(int32_t num, int32_t den);
  * key 11: 1 = never split K in echo_gemm_ws (the B = 1 runs that tests compare bitwise with B = 16 rows);
  * key 12: 1 = no small-M kernel in the auto pick (the round-3 small tiles; A/B);
  * key 13: group-M height of the persistent 256x256 and 320-row kernels' tile order (0 = 4; 1..64; bitwise-equal).
- * `tile` 100 + 10*C + S (C = small-M config 1..16, S = split 1..9) forces a small-M launch (tools/bench_gemm.py). */
+ * `tile` 100 + 10*C + S (C = small-M config 1..16, S = split 1..9) forces a small-M launch (tools/bench_gemm.py).
+ * The timing-ablation tiles 7-12 and 15 (results wrong) exist in the diagnostics build (ECHO_DIAG=1) only. */
 int echo_gemm_set_diag(int32_t key, int32_t value);
 
 /* One key/value segment of the joint attention (model.py:246-253): rows of
