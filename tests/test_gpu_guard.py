@@ -441,3 +441,51 @@ def test_no_store_past_end_codec(dtype):
     ca.check("rvq codes")
     qa.check("rvq z_q")
     la.check("rvq latents")
+
+
+# ------------------------------------------------------------------------------------- large-tile GEMMs
+@pytest.mark.parametrize("epi", ["store", "bias_silu", "swiglu", "resid", "headnorm", "f32out"])
+def test_no_store_past_end_gemm(epi):
+    """Every large-tile GEMM form — the 256x256 2-phase / persistent kernels (13 / 16 / 1), the smaller tile configs
+    (2-6), the 320-row tiles (20-23: auto DMA split, 4/5 split, one tile per workgroup, persistent), small-M configs
+    and the auto pick — on output rows with a 64-column gap after every row (ldc > output columns) and guards
+    before and after, at M with partial last tiles (700 rows: 2 x 320 + 60, 2 x 256 + 188). test_gpu_kernels.py
+    test_gemm_no_store_past_m checks the rows after M of contiguous outputs; this adds the row gaps, the front
+    guard, the 320-row forms and the head-norm / fp32 / bias epilogues."""
+    M, K = 700, 256
+    N = 1024
+    kind = {"store": L.EPI_STORE, "bias_silu": L.EPI_STORE, "swiglu": L.EPI_SWIGLU, "resid": L.EPI_RESID,
+            "headnorm": L.EPI_HEADNORM, "f32out": L.EPI_F32OUT}[epi]
+    nout = N // 2 if epi == "swiglu" else N
+    odt = torch.float32 if epi == "f32out" else BF
+    es = 4 if epi == "f32out" else 2
+    ldc = nout + 64
+    torch.manual_seed(11)
+    a = rnd(M, K)
+    w = rnd(N, K, scale=0.05)
+    bias = rnd(N, scale=0.1)
+    gate = (torch.rand(N, device=DEV) + 0.5).to(BF)
+    h0 = rnd(M, nout)
+    hw = (1 + 0.1 * torch.randn(8, 128, device=DEV)).to(BF)
+    rope = torch.randn(M, 64, 2, device=DEV)
+    ran = []
+    for tile in (0, 1, 2, 3, 4, 5, 6, 13, 16, 20, 21, 22, 23, 111, 131, 181):
+        ar = Arena(M * ldc * es)
+        out = ar.view(odt, (M, nout), (ldc, 1), fill=h0 if epi == "resid" else None)
+        g = _gemm_args(a, w, out.data_ptr(), ldc, kind, M, N, K, tile)
+        if epi == "bias_silu":
+            g.bias, g.act = bias.data_ptr(), L.ACT_SILU
+        if epi == "resid":
+            g.aux, g.ld_aux, g.gate = out.data_ptr(), ldc, gate.data_ptr()
+        if epi == "headnorm":
+            g.hn_w, g.hn_w_stride, g.hn_rope = hw.data_ptr(), 4 * 128, rope.data_ptr()
+            g.hn_heads, g.hn_nblk, g.hn_rope_heads, g.hn_seq_len, g.hn_pos0, g.hn_pos_mult, g.hn_eps = \
+                4, 2, 4, M, 0, 1, 1e-6
+        rc = lib().echo_gemm(C.byref(g), stream())
+        if rc == -1:  # ECHO_EINVAL: this config does not take the shape / epilogue
+            continue
+        ok(rc, f"echo_gemm tile {tile}")
+        ar.check(f"gemm {epi} tile {tile}")
+        assert torch.isfinite(out.float()).all(), tile
+        ran.append(tile)
+    assert len(ran) >= 8, ran
