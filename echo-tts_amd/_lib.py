@@ -80,6 +80,8 @@ SIGNATURES = {
     "echo_attention_pick_split": (i32, [C.POINTER(AttnArgs)]),
     "echo_attention_set_split": (i32, [i32]),
     "echo_attention_set_pipeline": (i32, [i32]),
+    "echo_set_sync_buffer": (i32, [vp, i64]),
+    "echo_attention_merge_in_launch": (i32, [C.POINTER(AttnArgs), i32]),
     "echo_rmsnorm": (i32, [i32, vp, i64, vp, vp, i64, i32, i32, f32, vp]),
     "echo_adaln_modulate": (i32, [i32, vp, vp, i32, i32, vp, vp, i32, i64, f32, vp]),
     "echo_head_norm_rope": (i32, [i32, vp, i64, i32, i32, i32, i64, i64, vp, i64, vp, i32, i32, i32, i32,

@@ -176,6 +176,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t attn_rsrc(const void* p, uint3
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
+// write-through (sc1) stores of the in-launch split-KV merge (SP = 2): the line leaves this XCD's L2 on the store,
+// so the merging workgroup on any XCD reads it after its acquire (cdna_hip_programming.md Guideline 16, R1)
+constexpr int ATTN_SYNC_ERR = 0;   // sync word 0: set when a bounded poll gave up (never in a correct run)
+constexpr int ATTN_SYNC_CNT0 = 16;  // the per-item [arrivals, departures] counters start at word 16
+__device__ __forceinline__ void st_sc1_b128(const __amdgpu_buffer_rsrc_t& rs, uint32_t off, float4 v) {
+  typedef __attribute__((__vector_size__(4 * sizeof(float)))) float f32v4;
+  __builtin_amdgcn_raw_buffer_store_b128((f32v4){v.x, v.y, v.z, v.w}, rs, off, 0, 16);
+}
+__device__ __forceinline__ void st_sc1_b64(float* p, float2 v) {
+  const uint64_t bits = ((uint64_t)__float_as_uint(v.y) << 32) | __float_as_uint(v.x);
+  __hip_atomic_store((uint64_t*)p, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // 8 16-B stores per valid lane (a wave with any valid lane issues exactly 8 store instructions)
 __device__ __forceinline__ void attn_write_out(const uint4 (&v4)[8], bf16_t* op, int h2, bool valid) {
   if (!valid) return;
@@ -270,11 +283,19 @@ struct SegInfo {
 // the item's flat tile list and stores its UNNORMALISED partial (O fp32, m in exp2 units, l) to
 // `ws` (layout: attn_split_ws_bytes); attn_combine_kernel merges the splits, normalises, gates and
 // stores. Same tile math; only the summation order over keys differs from SP = 0 (fp32-close).
+// SP = 2: the same split, merged inside the launch (no attn_combine_kernel): each split publishes its partial
+// with write-through (sc1) stores, every storing wave drains, one lane adds to the item's arrival counter in
+// `sync` and polls it (relaxed, bounded) until all nsp splits have arrived, then ONE agent-scope acquire and
+// the workgroup merges its 1/nsp share of the item's (query, 8-column) units with attn_combine_unit — the
+// combine kernel's arithmetic, so the output is bitwise the SP = 1 + combine result (cdna_hip_programming.md
+// Guideline 16, R1 / counter form). Needs every split of an item resident at once: the host launches it only
+// for grids of at most one workgroup per CU. The last split to depart resets the item's two counters, so
+// `sync` (caller-owned, zero at first use) is zero again when the launch ends.
 template <int ABL, int NW, int ST, int KTT = 64, int PS = 0, int SP = 0>
 __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
-    attn_bf16_kernel(EchoAttnArgs a_arg, float* ws, int nsp) {
+    attn_bf16_kernel(EchoAttnArgs a_arg, float* ws, int nsp, uint32_t* sync) {
   static_assert(!PS || (ABL == 0 && ST == 2), "persistent form: production schedule only");
-  static_assert(!SP || (ABL == 0 && ST == 2 && !PS), "split-KV form: production schedule only");
+  static_assert(!SP || (ABL == 0 && ST == 2 && !PS && NW == 4), "split-KV form: production schedule only");
   constexpr int QB = 32 * NW;
   constexpr int DPT = KTT / (4 * NW);  // DMA wave-instructions per wave per K (or V) tile
   const uint64_t ts0 = (ABL & 128) ? rt_now() : 0;
@@ -293,6 +314,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
   const int nitems = PS ? nqb * kargs->rows * kargs->heads : (int)blockIdx.x + 1;
   (void)ws;
   (void)nsp;
+  (void)sync;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h2 = lane >> 5, ql = lane & 31;
@@ -627,23 +649,65 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
     if constexpr (SP) {
       // partial O at chunk c = d / 4 (32 chunks of 4 floats), laid out [chunk][query] so the 32
       // lanes of a half-wave store 512 contiguous bytes per instruction
+      const int64_t it = ((int64_t)sp * a.rows + row) * a.heads + head;
+      const int64_t ml_off = (int64_t)nsp * a.rows * a.heads * 128 * a.n_q;  // (m, l) pairs after every O
+      const __amdgpu_buffer_rsrc_t wsr = attn_rsrc(ws, 0xFFFFFFF0u);  // SP = 2: the O partials' byte offsets
+      (void)wsr;
       if (valid) {
-        const int64_t it = ((int64_t)sp * a.rows + row) * a.heads + head;
         float* wo = ws + it * 128 * a.n_q;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
           for (int rg = 0; rg < 4; ++rg) {
             const int c = dt * 8 + 2 * rg + h2;
-            *(float4*)(wo + ((int64_t)c * a.n_q + qi) * 4) =
-                make_float4(o[dt][4 * rg], o[dt][4 * rg + 1], o[dt][4 * rg + 2], o[dt][4 * rg + 3]);
+            const float4 v = make_float4(o[dt][4 * rg], o[dt][4 * rg + 1], o[dt][4 * rg + 2], o[dt][4 * rg + 3]);
+            if constexpr (SP == 2) {
+              st_sc1_b128(wsr, (uint32_t)(((it * 128 + (int64_t)c * 4) * a.n_q + (int64_t)qi * 4) * 4), v);
+            } else {
+              *(float4*)(wo + ((int64_t)c * a.n_q + qi) * 4) = v;
+            }
           }
         if (h2 == 0) {
-          float* wml = ws + (int64_t)nsp * a.rows * a.heads * 128 * a.n_q + (it * a.n_q + qi) * 2;
-          *(float2*)wml = make_float2(m_run == -INFINITY ? -INFINITY : m_run * sl2, lt);
+          float* wml = ws + ml_off + (it * a.n_q + qi) * 2;
+          const float2 v = make_float2(m_run == -INFINITY ? -INFINITY : m_run * sl2, lt);
+          if constexpr (SP == 2) st_sc1_b64(wml, v); else *(float2*)wml = v;
         }
       }
       (void)inv;
+      if constexpr (SP == 2) {
+        // publish: every storing wave drains its write-through stores, then one arrival per workgroup
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const int rh = row * a.heads + head;
+        uint32_t* cnt = sync + ATTN_SYNC_CNT0 + 2 * ((int64_t)rh * nqb + qb);  // [arrivals, departures] of this item
+        if (tid == 0) {
+          __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          uint32_t spins = 0;
+          while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)nsp) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins == (1u << 22)) {  // bounded: never hang the GPU; the error word tells the host
+              __hip_atomic_store(sync + ATTN_SYNC_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        // this split's share of the item's QB x 16 (query, 8-column) units, 16 queries x 16 chunks per pass
+        constexpr int U = QB * 16;
+        const int u0 = sp * U / nsp, u1 = (sp + 1) * U / nsp;
+        for (int u = u0 + tid; u < u1; u += 64 * NW) {
+          const int qq = q0 + (u & 15) + 16 * (u >> 8), c8 = (u >> 4) & 15;
+          if (qq < a.n_q) attn_combine_unit(a, ws, nsp, rh, qq, c8);
+        }
+        // depart: the last split to leave finds every other split past its poll and re-zeroes the counters
+        if (tid == 0 && __hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                            (uint32_t)nsp - 1) {
+          __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
     } else if constexpr (PS) {
       // (the persistent form keeps the per-lane epilogue: the row form's LDS transposition needs a
       // barrier before the next item's DMA and spills around the item loop — 179 vs 154 us, R = 16)
@@ -1411,7 +1475,7 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
   const int qb = (cfg == 1 || cfg == 2 || cfg == 4) ? 256 : 128;
   const dim3 grid(attn_grid(a, qb));
   if (cfg == 0 && abl == 0) {
-    hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1);
+    hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), grid, dim3(256), 0, s, *a, (float*)nullptr, 1, (uint32_t*)nullptr);
     ECHO_LAUNCH_CHECK();
     return 0;
   }
@@ -1426,7 +1490,7 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
   return ECHO_EINVAL;
 #else
 #define ECHO_ATTN_LAUNCH(A, NW, ST, ...) \
-  hipLaunchKernelGGL((attn_bf16_kernel<A, NW, ST, ##__VA_ARGS__>), grid, dim3(64 * NW), 0, s, *a, (float*)nullptr, 1)
+  hipLaunchKernelGGL((attn_bf16_kernel<A, NW, ST, ##__VA_ARGS__>), grid, dim3(64 * NW), 0, s, *a, (float*)nullptr, 1, (uint32_t*)nullptr)
 #define ECHO_ATTN_ABLS(NW, ST)                        \
   switch (abl) {                                      \
     case 0: ECHO_ATTN_LAUNCH(0, NW, ST); break;       \
@@ -1458,13 +1522,13 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       if (abl) return ECHO_EINVAL;
       const int ps_grid = attn_ps_grid(grid.x);
       if (ps_grid <= 0) return ECHO_EINVAL;
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a, (float*)nullptr, 1);
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 1>), dim3(ps_grid), dim3(256), 0, s, *a, (float*)nullptr, 1, (uint32_t*)nullptr);
       break;
     }
     case 6: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 2, 32); break;
     case 9:  // 2 waves x 32 queries per workgroup
       if (abl) return ECHO_EINVAL;
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 2, 2>), dim3(attn_grid(a, 64)), dim3(128), 0, s, *a, (float*)nullptr, 1);
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 2, 2>), dim3(attn_grid(a, 64)), dim3(128), 0, s, *a, (float*)nullptr, 1, (uint32_t*)nullptr);
       break;
     case 7: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(0, 4, 3, 32); break;
     case 10: if (abl) return ECHO_EINVAL; ECHO_ATTN_LAUNCH(2048, 4, 2); break;  // per-lane epilogue
@@ -1541,7 +1605,7 @@ extern "C" int echo_attention(const EchoAttnArgs* a, void* stream) {
     if (g_attn_pl && !any_causal(a))
       hipLaunchKernelGGL(attn_pl_kernel<0>, dim3(attn_grid(a, 128)), dim3(256), 0, s, *a);
     else
-      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1);
+      hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2>), dim3(attn_grid(a, 128)), dim3(256), 0, s, *a, (float*)nullptr, 1, (uint32_t*)nullptr);
   } else {
     hipLaunchKernelGGL(attn_f32_kernel, dim3(attn_grid(a, FQ)), dim3(64), 0, s, *a);
   }
@@ -1610,6 +1674,26 @@ extern "C" int echo_attention_set_split(int32_t nsplit) {
   return 0;
 }
 
+namespace {
+uint32_t* g_sync = nullptr;  // echo_set_sync_buffer: caller-owned counters of in-launch merges (0 words = off)
+int64_t g_sync_words = 0;
+}  // namespace
+
+extern "C" int echo_set_sync_buffer(uint32_t* sync, int64_t words) {
+  if ((sync == nullptr) != (words == 0) || words < 0 || (uintptr_t)sync % 64) return ECHO_EINVAL;
+  g_sync = sync;
+  g_sync_words = words;
+  return 0;
+}
+
+extern "C" int32_t echo_attention_merge_in_launch(const EchoAttnArgs* a, int32_t nsplit) {
+  if (!g_sync || !a || nsplit < 2 || nsplit > 16 || a->rows <= 0 || a->heads <= 0 || a->n_q <= 0) return 0;
+  const int64_t items = (int64_t)attn_grid(a, 128);
+  // every split of an item must be resident at once: at most one workgroup per CU; counters must fit
+  return items * nsplit <= cu_count() && ATTN_SYNC_CNT0 + 2 * items <= g_sync_words &&
+         echo_attention_split_ws_bytes(a, nsplit) < ((int64_t)1 << 32) - 16;
+}
+
 extern "C" int echo_attention_split(const EchoAttnArgs* a, int32_t nsplit, void* ws, int64_t ws_bytes, void* stream) {
   const int rc = check_attn_args(a);
   if (rc) return rc;
@@ -1618,8 +1702,14 @@ extern "C" int echo_attention_split(const EchoAttnArgs* a, int32_t nsplit, void*
   if (nsplit > 16) return ECHO_EINVAL;
   if (!ws || (uintptr_t)ws % 16 || ws_bytes < echo_attention_split_ws_bytes(a, nsplit)) return ECHO_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  if (echo_attention_merge_in_launch(a, nsplit)) {  // one launch: the splits merge themselves (SP = 2)
+    hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 0, 2>), dim3(attn_grid(a, 128) * nsplit), dim3(256), 0, s, *a,
+                       (float*)ws, (int)nsplit, g_sync);
+    ECHO_LAUNCH_CHECK();
+    return 0;
+  }
   hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 0, 1>), dim3(attn_grid(a, 128) * nsplit), dim3(256), 0, s, *a,
-                     (float*)ws, (int)nsplit);
+                     (float*)ws, (int)nsplit, (uint32_t*)nullptr);
   ECHO_LAUNCH_CHECK();
   hipLaunchKernelGGL(attn_combine_kernel, dim3(a->rows * a->heads * ((a->n_q + 15) / 16)), dim3(256), 0, s, *a,
                      (const float*)ws, (int)nsplit);

@@ -35,6 +35,11 @@ INIT_SCALE = 0.999  # inference.py:470
 #   C5, 16 x 160-latent blocks: 2 x 8 is 6.4 % slower (M = 3840 per launch is too small to fill the chip).
 STREAM_SPLIT_MIN_TOKENS = int(os.environ.get("ECHO_STREAM_SPLIT_MIN_TOKENS", "0"))
 
+# Split-KV attention of the under-filled launches (B = 1, blockwise blocks) merges its splits inside the split
+# launch (ops.in_launch_sync with a per-plan counter buffer) instead of a separate combine pass: one launch fewer
+# per attention, bitwise the same output. ECHO_INLAUNCH_MERGE=0 turns it off (A/B).
+INLAUNCH_MERGE = os.environ.get("ECHO_INLAUNCH_MERGE", "1") != "0"
+
 
 @dataclass(frozen=True)
 class Schedule:
@@ -149,6 +154,8 @@ class CFGPlan:
         self.lens = torch.zeros((4, 3 * B), device=dev, dtype=torch.int32)  # text3, spk3, text1, spk1
         self.kv_scale, self.kv_cols = kv_scale, kv_scale_cols(model, kv_max_layers)
         self.args = [step_args(a) for a in sched.args]
+        # this plan's in-launch merge counters (its launches never run concurrently with each other)
+        self.sync = ops.new_sync_buffer(dev) if INLAUNCH_MERGE else None
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.runs = 0
 
@@ -225,12 +232,13 @@ class CFGPlan:
         if use_graph and self.graph is not None:
             self.graph.replay()
         else:
-            self.loop()
-            if use_graph:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self.loop()
-                self.graph = g
+            with ops.in_launch_sync(self.sync):
+                self.loop()
+                if use_graph:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        self.loop()
+                    self.graph = g
         self.runs += 1
         return self.output()
 
@@ -249,7 +257,8 @@ class CFGPlan:
         ws = self.ws.view(copies * self.B * self.N)
         ops.latent_to_input(xs, ws.xin, copies)
         seg = self._segs(self.sched.has_cfg[i])
-        self.m.decoder(ws, copies * self.B, self.N, self.table[i], seg, 0, copies=copies)
+        with ops.in_launch_sync(self.sync):
+            self.m.decoder(ws, copies * self.B, self.N, self.table[i], seg, 0, copies=copies)
         return ws.v.view(copies * self.B, self.N, -1).clone()
 
 
@@ -350,8 +359,9 @@ class BlockPlan(CFGPlan):
         copies = 3 if self.sched.has_cfg[i] else 1
         ws = self.ws.view(copies * self.B * bs)
         ops.latent_to_input(xs, ws.xin, copies)
-        self.m.decoder(ws, copies * self.B, bs, self.table[i], seg_cfg if self.sched.has_cfg[i] else seg_plain,
-                       self.starts[b], copies=copies)
+        with ops.in_launch_sync(self.sync):
+            self.m.decoder(ws, copies * self.B, bs, self.table[i], seg_cfg if self.sched.has_cfg[i] else seg_plain,
+                           self.starts[b], copies=copies)
         return ws.v.view(copies * self.B, bs, -1).clone()
 
 

@@ -203,6 +203,49 @@ def attention_pipeline(mode):
     return _knob("attention_pipeline", int(mode))
 
 
+# In-launch merges (echo_set_sync_buffer): a zeroed int32 buffer of counters, one per captured plan (never shared by
+# launches that can run at the same time); every launch that uses it leaves it zero again.
+SYNC_WORDS = 4096
+_SYNC: Optional[Tensor] = None
+
+
+def new_sync_buffer(device) -> Tensor:
+    """A fresh counter buffer for `in_launch_sync` (zero; 16 KiB)."""
+    return torch.zeros(SYNC_WORDS, dtype=torch.int32, device=device)
+
+
+def _set_sync(buf: Optional[Tensor]) -> None:
+    global _SYNC
+    if buf is None:
+        rc = lib().echo_set_sync_buffer(None, 0)
+    else:
+        if not (buf.is_cuda and buf.dtype == torch.int32 and buf.is_contiguous() and buf.data_ptr() % 64 == 0):
+            raise ValueError("in_launch_sync: a contiguous, 64-B aligned int32 device buffer is required")
+        rc = lib().echo_set_sync_buffer(buf.data_ptr(), buf.numel())
+    if rc:
+        raise RuntimeError(f"echo_set_sync_buffer refused: {L.ERRORS.get(rc, rc)}")
+    _SYNC = buf
+
+
+@contextlib.contextmanager
+def in_launch_sync(buf: Optional[Tensor]):
+    """Inside the block, split-KV attention launches whose splits can all be resident merge them inside the
+    launch (one kernel instead of split + combine, bitwise the same output), with `buf`'s counters
+    (echo_set_sync_buffer; None = off). The engine's plans run and capture their step loop inside this block
+    with their own buffer; restores the previous buffer on exit."""
+    prev = _SYNC
+    _set_sync(buf)
+    try:
+        yield
+    finally:
+        _set_sync(prev)
+
+
+def sync_errors(buf: Tensor) -> int:
+    """Word 0 of a counter buffer: non-zero if a bounded in-launch wait ever gave up (never in a correct run)."""
+    return int(buf[0].item())
+
+
 @contextlib.contextmanager
 def policy_rows(num: int, den: int):
     """Split decisions (GEMM split-K, attention split-KV) taken for num / den times each launch's rows

@@ -251,6 +251,13 @@ def test_gemm_small_m_plan_host_policy(lib):
     assert lib.echo_attention_set_pipeline(0) == 0 and lib.echo_attention_set_pipeline(1) == 0
     if " diag " not in lib.echo_version().decode():  # attn_w64_kernel: diagnostics build only
         assert lib.echo_attention_set_pipeline(2) == -1  # ECHO_EINVAL
+    # in-launch merge counters: NULL/0 = off; a buffer must be 64-B aligned and sized; host-only checks
+    assert lib.echo_set_sync_buffer(None, 0) == 0
+    assert lib.echo_set_sync_buffer(fake + 4, 4096) != 0 and lib.echo_set_sync_buffer(None, 16) != 0
+    assert lib.echo_set_sync_buffer(fake, 0) != 0
+    assert lib.echo_attention_merge_in_launch(None, 3) == 0
+    assert lib.echo_set_sync_buffer(fake, 4096) == 0  # (its grid / residency rule: test_gpu_kernels.py policy test)
+    assert lib.echo_set_sync_buffer(None, 0) == 0
 
 
 def test_asm_owned_attention_registers_untouched():

@@ -125,12 +125,15 @@ def _attn_case(kind, dtype):
     return segs, R, n_q, H, qkvg[:, :, 0], qkvg[:, :, 3], (qkvg, kt, tl)
 
 
-@pytest.mark.parametrize("kind,dtype,nsplit", [("plain", BF, 1), ("small", BF, 1), ("causal", BF, 1),
-                                               ("plain", torch.float32, 1), ("plain", BF, 3), ("small", BF, 16),
-                                               ("causal", BF, 4)])
-def test_no_store_past_end_attention(kind, dtype, nsplit):
+@pytest.mark.parametrize("kind,dtype,nsplit,merge", [("plain", BF, 1, False), ("small", BF, 1, False),
+                                                     ("causal", BF, 1, False), ("plain", torch.float32, 1, False),
+                                                     ("plain", BF, 3, False), ("small", BF, 16, False),
+                                                     ("causal", BF, 4, False), ("plain", BF, 3, True),
+                                                     ("small", BF, 8, True), ("causal", BF, 4, True)])
+def test_no_store_past_end_attention(kind, dtype, nsplit, merge):
     """Attention output rows with a gap after each token (o_ld_tok > heads x 128) and after each batch row's n_q
-    queries (stores of queries past n_q would land there); split-KV: the exact-size workspace too."""
+    queries (stores of queries past n_q would land there); split-KV: the exact-size workspace too; merged
+    inside the launch: the counter buffer as well (its counters back to zero, nothing past its words)."""
     segs, R, n_q, H, q, gate, keep = _attn_case(kind, dtype)
     es = 2 if dtype == BF else 4
     o_ld_tok = H * 128 + 64
@@ -145,8 +148,19 @@ def test_no_store_past_end_attention(kind, dtype, nsplit):
         assert wsb > 0
         wa = Arena(wsb)
         ws = wa.view(torch.uint8, (wsb,))
-        ok(lib().echo_attention_split(C.byref(a), nsplit, ws.data_ptr(), wsb, stream()), "echo_attention_split")
+        sa = Arena(4096 * 4)
+        sync = sa.view(torch.int32, (4096,), fill=torch.zeros(4096, dtype=torch.int32, device=DEV))
+        if merge:
+            ok(lib().echo_set_sync_buffer(sync.data_ptr(), 4096), "echo_set_sync_buffer")
+        try:
+            if merge:
+                assert lib().echo_attention_merge_in_launch(C.byref(a), nsplit) == 1
+            ok(lib().echo_attention_split(C.byref(a), nsplit, ws.data_ptr(), wsb, stream()), "echo_attention_split")
+        finally:
+            lib().echo_set_sync_buffer(None, 0)
         wa.check("split-KV workspace")
+        sa.check("in-launch merge counters")
+        assert int(sync.abs().sum()) == 0, "counters not reset"
     ar.check(f"attention {kind} nsplit={nsplit}")
     assert torch.isfinite(out.float()).all()
 

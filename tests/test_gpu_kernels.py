@@ -487,6 +487,65 @@ def test_attention_split_kv(nsplit, R, n_q):
     split_close(got, ref, ref_attention(qkvg[:, :, 0], segs, qkvg[:, :, 3], 128 ** -0.5, BF))
 
 
+@pytest.mark.parametrize("nsplit", [2, 3, 4, 8, 16])
+@pytest.mark.parametrize("R,n_q,causal", [(1, 640, False), (3, 640, False), (3, 160, False), (1, 37, False),
+                                          (1, 333, True)])
+def test_attention_split_merge_in_launch_bitwise(nsplit, R, n_q, causal):
+    """Split-KV with the splits merged inside the launch (ops.in_launch_sync: write-through partials, arrival
+    counters, the combine's arithmetic per query and 8 columns) is bitwise the split kernel + combine pass; every
+    launch leaves the counter buffer zero (the next one starts clean), repeated and graph-replayed launches
+    agree, and no bounded wait gave up (word 0)."""
+    if causal:
+        qkv = torch.randn(R, n_q, 4, 3, 128, device=DEV).to(BF)
+        q, gate, segs = qkv[:, :, 0], None, [ops.Segment(qkv[:, :, 1], qkv[:, :, 2], causal=True)]
+    else:
+        qkvg, segs = _small_batch_segments(1, R, n_q, H=4, tl_valid=271)
+        q, gate = qkvg[:, :, 0], qkvg[:, :, 3]
+    H = q.shape[2]
+    ref = torch.full((R, n_q, H, 128), float("nan"), device=DEV, dtype=BF)
+    with ops.attention_split(nsplit):
+        ops.attention(q, segs, out=ref, gate=gate)  # split kernel + attn_combine_kernel
+    buf = ops.new_sync_buffer(DEV)
+    got = torch.full_like(ref, float("nan"))
+    with ops.attention_split(nsplit), ops.in_launch_sync(buf):
+        assert ops.lib().echo_attention_merge_in_launch(None, nsplit) == 0
+        for _ in range(3):  # counters reset by every launch
+            got.fill_(float("nan"))
+            ops.attention(q, segs, out=got, gate=gate)
+            torch.cuda.synchronize()
+            assert torch.equal(got, ref), float((got.float() - ref.float()).abs().max())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            ops.attention(q, segs, out=got, gate=gate)
+    for _ in range(2):
+        got.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref)
+    assert int(buf.abs().sum()) == 0, "counters left non-zero"
+    assert ops.sync_errors(buf) == 0
+
+
+def test_attention_merge_in_launch_policy():
+    """The in-launch merge is taken only while a counter buffer is set and only for grids of at most one
+    workgroup per CU (every split of an item resident at once); otherwise the two-kernel form runs."""
+    qkvg, segs = _small_batch_segments(1, 1, 640, H=16, tl_valid=300)
+    buf = ops.new_sync_buffer(DEV)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    a = L.AttnArgs()
+    a.dtype, a.rows, a.n_q, a.heads, a.nseg = 0, 1, 640, 16, 1
+    a.q = qkvg.data_ptr()
+    lib_ = ops.lib()
+    items = 5 * 16  # 640 queries = 5 blocks of 128, x 16 heads, x 1 row
+    assert lib_.echo_attention_merge_in_launch(a, 3) == 0          # no buffer set
+    with ops.in_launch_sync(buf):
+        for nsp in (2, 3, 4, 8):
+            assert lib_.echo_attention_merge_in_launch(a, nsp) == int(items * nsp <= cus), nsp
+        a.rows = 3
+        assert lib_.echo_attention_merge_in_launch(a, 2) == int(3 * items * 2 <= cus)
+    assert lib_.echo_attention_merge_in_launch(a, 2) == 0
+
+
 @pytest.mark.parametrize("L_", [37, 160, 333])
 def test_attention_split_kv_causal(L_):
     """Split-KV on a causal (encoder) segment: queries whose split holds no visible key."""
