@@ -176,14 +176,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t attn_rsrc(const void* p, uint3
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-// write-through (sc1) stores of the in-launch split-KV merge (SP = 2): the line leaves this XCD's L2 on the store,
-// so the merging workgroup on any XCD reads it after its acquire (cdna_hip_programming.md Guideline 16, R1)
-constexpr int ATTN_SYNC_ERR = 0;   // sync word 0: set when a bounded poll gave up (never in a correct run)
-constexpr int ATTN_SYNC_CNT0 = 16;  // the per-item [arrivals, departures] counters start at word 16
-__device__ __forceinline__ void st_sc1_b128(const __amdgpu_buffer_rsrc_t& rs, uint32_t off, float4 v) {
-  typedef __attribute__((__vector_size__(4 * sizeof(float)))) float f32v4;
-  __builtin_amdgcn_raw_buffer_store_b128((f32v4){v.x, v.y, v.z, v.w}, rs, off, 0, 16);
-}
+// 8-B write-through store of the in-launch split-KV merge's (m, l) pair (common.h: the 16-B form, the protocol)
 __device__ __forceinline__ void st_sc1_b64(float* p, float2 v) {
   const uint64_t bits = ((uint64_t)__float_as_uint(v.y) << 32) | __float_as_uint(v.x);
   __hip_atomic_store((uint64_t*)p, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -651,7 +644,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
       // lanes of a half-wave store 512 contiguous bytes per instruction
       const int64_t it = ((int64_t)sp * a.rows + row) * a.heads + head;
       const int64_t ml_off = (int64_t)nsp * a.rows * a.heads * 128 * a.n_q;  // (m, l) pairs after every O
-      const __amdgpu_buffer_rsrc_t wsr = attn_rsrc(ws, 0xFFFFFFF0u);  // SP = 2: the O partials' byte offsets
+      const __amdgpu_buffer_rsrc_t wsr = rsrc_of(ws, 0xFFFFFFF0u);  // SP = 2: the O partials' byte offsets
       (void)wsr;
       if (valid) {
         float* wo = ws + it * 128 * a.n_q;
@@ -679,20 +672,8 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         const int rh = row * a.heads + head;
-        uint32_t* cnt = sync + ATTN_SYNC_CNT0 + 2 * ((int64_t)rh * nqb + qb);  // [arrivals, departures] of this item
-        if (tid == 0) {
-          __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          uint32_t spins = 0;
-          while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)nsp) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins == (1u << 22)) {  // bounded: never hang the GPU; the error word tells the host
-              __hip_atomic_store(sync + ATTN_SYNC_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-          }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        uint32_t* cnt = sync + SYNC_CNT0 + 2 * ((int64_t)rh * nqb + qb);  // [arrivals, departures] of this item
+        if (tid == 0) sync_arrive_wait(sync, cnt, (uint32_t)nsp);
         __syncthreads();
         // this split's share of the item's QB x 16 (query, 8-column) units, 16 queries x 16 chunks per pass
         constexpr int U = QB * 16;
@@ -701,12 +682,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
           const int qq = q0 + (u & 15) + 16 * (u >> 8), c8 = (u >> 4) & 15;
           if (qq < a.n_q) attn_combine_unit(a, ws, nsp, rh, qq, c8);
         }
-        // depart: the last split to leave finds every other split past its poll and re-zeroes the counters
-        if (tid == 0 && __hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                            (uint32_t)nsp - 1) {
-          __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (tid == 0) sync_depart(cnt, (uint32_t)nsp);
       }
     } else if constexpr (PS) {
       // (the persistent form keeps the per-lane epilogue: the row form's LDS transposition needs a
@@ -1674,10 +1650,8 @@ extern "C" int echo_attention_set_split(int32_t nsplit) {
   return 0;
 }
 
-namespace {
 uint32_t* g_sync = nullptr;  // echo_set_sync_buffer: caller-owned counters of in-launch merges (0 words = off)
 int64_t g_sync_words = 0;
-}  // namespace
 
 extern "C" int echo_set_sync_buffer(uint32_t* sync, int64_t words) {
   if ((sync == nullptr) != (words == 0) || words < 0 || (uintptr_t)sync % 64) return ECHO_EINVAL;
@@ -1690,7 +1664,7 @@ extern "C" int32_t echo_attention_merge_in_launch(const EchoAttnArgs* a, int32_t
   if (!g_sync || !a || nsplit < 2 || nsplit > 16 || a->rows <= 0 || a->heads <= 0 || a->n_q <= 0) return 0;
   const int64_t items = (int64_t)attn_grid(a, 128);
   // every split of an item must be resident at once: at most one workgroup per CU; counters must fit
-  return items * nsplit <= cu_count() && ATTN_SYNC_CNT0 + 2 * items <= g_sync_words &&
+  return items * nsplit <= cu_count() && SYNC_CNT0 + 2 * items <= g_sync_words &&
          echo_attention_split_ws_bytes(a, nsplit) < ((int64_t)1 << 32) - 16;
 }
 

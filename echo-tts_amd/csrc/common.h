@@ -89,6 +89,47 @@ __device__ __forceinline__ float silu_bf16in(float a) {
   return a == 5.9375f ? 5.90625f : s;
 }
 
+// ---- in-launch hand-offs between workgroups of one launch (cdna_hip_programming.md Guideline 16: write-through
+// (sc1) payload stores drained by every storing wave, one relaxed agent-scope arrival per workgroup, a relaxed
+// bounded poll, ONE agent-scope acquire) over the caller-owned counter buffer of echo_set_sync_buffer: word 0 is
+// the error flag (a bounded poll gave up: never in a correct run), the [arrivals, departures] pairs start at
+// word 16. Every workgroup that waits must be resident at once: the host launches these forms only for grids of
+// at most one workgroup per CU.
+constexpr int SYNC_ERR = 0, SYNC_CNT0 = 16;
+extern uint32_t* g_sync;      // echo_set_sync_buffer (attention.hip); NULL = in-launch hand-offs off
+extern int64_t g_sync_words;
+// ONE lane, after every storing wave's s_waitcnt vmcnt(0) and a workgroup barrier; the workgroup joins another
+// barrier after it before any load of the handed-off bytes
+__device__ __forceinline__ void sync_arrive_wait(uint32_t* sync, uint32_t* cnt, uint32_t expect) {
+  __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t spins = 0;
+  while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < expect) {
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins == (1u << 22)) {  // bounded: never hang the GPU
+      __hip_atomic_store(sync + SYNC_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// ONE lane of a workgroup that passed sync_arrive_wait on `cnt`: the last of the n departures finds every
+// waiter past its poll and re-zeroes the pair (the buffer is zero again when the launch ends)
+__device__ __forceinline__ void sync_depart(uint32_t* cnt, uint32_t n) {
+  if (__hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1) {
+    __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// 16-B write-through store at a byte offset of a buffer resource (aux 16 = sc1)
+__device__ __forceinline__ void st_sc1_b128(const __amdgpu_buffer_rsrc_t& rs, uint32_t off, float4 v) {
+  typedef __attribute__((__vector_size__(4 * sizeof(float)))) float f32v4;
+  __builtin_amdgcn_raw_buffer_store_b128((f32v4){v.x, v.y, v.z, v.w}, rs, off, 0, 16);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -40,6 +40,8 @@ struct Epi {
   int conv_c, conv_taps, conv_dil;  // causal-conv A addressing (echo_hip.h)
   // RESID + the next AdaLN (EchoGemmArgs.mod_*; the split-K finish kernel only)
   void* mod_out; int64_t ld_mod; const void* mod_shift; const void* mod_scale1; float mod_eps;
+  // EK_PARTIAL_FUSED (the split-K finish inside the launch): the output, its row stride, the counter buffer
+  void* fin_out; int64_t fin_ldc; uint32_t* sync;
 };
 
 // Element offset added to A for the K-slice starting at k0 in conv mode (0 otherwise): tap
@@ -503,6 +505,13 @@ gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
 //          straight from registers: 16 B per lane), and gemm_splitk_finish_kernel sums the S slabs in
 //          order s = 0 .. S-1 and applies the epilogue.
 constexpr int EK_PARTIAL = 6;
+// EK_PARTIAL_FUSED (gated residual only, round 6): the K-slices of a tile store their slabs write-through, wait for
+// each other (per-tile arrival counter in the caller's counter buffer, common.h), and each finishes 1/S of the
+// tile's (row, 8-column) units with gemm_splitk_finish_kernel<EK_RESID>'s arithmetic; with ep.mod_out the row
+// panel's workgroups then wait for the whole panel and each normalises + modulates a share of its rows, one wave per
+// row, with the finish kernel's MOD arithmetic (= adaln_rows_kernel<4>'s). One launch instead of GEMM + finish,
+// bitwise the same output. Every workgroup of the launch must be resident at once (host: grid <= CUs).
+constexpr int EK_PARTIAL_FUSED = 7;
 
 // vmcnt(n * D) for n = 0 .. 3 (counted waits need immediates)
 template <int D>
@@ -511,6 +520,98 @@ __device__ __forceinline__ void vm_wait_stages(int n) {
   else if (n == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory");
   else if (n == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// The in-launch split-K finish of EK_PARTIAL_FUSED (see there). ws: the S fp32 slabs [S][M][N]; this workgroup is
+// K-slice s of tile (tm, tn) with origin (m0, n0).
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void sk_fused_finish(const void* ws, int M, int N, int S, int s, int tm, int tn, int tiles_m,
+                                                int tiles_n, int m0, int n0, const Epi& ep) {
+  uint32_t* sync = ep.sync;
+  const bool mod = ep.mod_out != nullptr;
+  // publish this K-slice's slab tile (every storing wave drained its write-through stores), wait for the tile's S
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  uint32_t* tcnt = sync + SYNC_CNT0 + 2 * (tm * tiles_n + tn);
+  if (threadIdx.x == 0) sync_arrive_wait(sync, tcnt, (uint32_t)S);
+  __syncthreads();
+  // 1/S of the tile's (row, 8-column) units, gemm_splitk_finish_kernel<EK_RESID>'s arithmetic
+  constexpr int CPR = BN / 8, U = BM * CPR;
+  const float* ws0 = (const float*)ws;
+  const int64_t slab = (int64_t)M * N;
+  const __amdgpu_buffer_rsrc_t hr = rsrc_of(ep.fin_out, 0xFFFFFFF0u);
+  (void)hr;
+  for (int u = s * U / S + (int)threadIdx.x; u < (s + 1) * U / S; u += NT) {
+    const int r = u / CPR, c = u - r * CPR;
+    const int m = m0 + r, n = n0 + 8 * c;
+    if (m >= M) continue;
+    float v[8];
+    load8(ws0 + (int64_t)m * N + n, v);
+    for (int k = 1; k < S; ++k) {
+      float w[8];
+      load8(ws0 + k * slab + (int64_t)m * N + n, w);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += w[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = rbf(v[e]);
+    float x[8];
+    load8((const bf16_t*)ep.aux + (int64_t)m * ep.ld_aux + n, x);
+    if (ep.gate) {
+      float g[8];
+      load8((const bf16_t*)ep.gate + n, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = rbf(g[e] * v[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = x[e] + v[e];  // the store rounds
+    if (mod) {  // the panel's other workgroups read this row: write-through
+      const uint4 h = make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+      st_sc1_b128(hr, (uint32_t)(((int64_t)m * ep.fin_ldc + n) * 2),
+                  make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w)));
+    } else {
+      store8((bf16_t*)ep.fin_out + (int64_t)m * ep.fin_ldc + n, v);
+    }
+  }
+  if (threadIdx.x == 0) sync_depart(tcnt, (uint32_t)S);
+  if (!mod) return;
+  // the next AdaLN needs whole rows: wait for every K-slice of every column tile of this row panel
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int pw = tiles_n * S;  // workgroups of the panel
+  uint32_t* pcnt = sync + SYNC_CNT0 + 2 * (tiles_m * tiles_n + tm);
+  if (threadIdx.x == 0) sync_arrive_wait(sync, pcnt, (uint32_t)pw);
+  __syncthreads();
+  // one wave per row: rows k, k + pw, ... of the panel for this workgroup's index k; lane l holds the 8-column
+  // chunks t = q * 64 + l (q = 0..3), squares summed in (q, e) order, then the wave butterfly (the finish MOD)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int NWV = NT / 64;
+  for (int r = tn * S + s + wv * pw; r < BM; r += NWV * pw) {
+    const int m = m0 + r;
+    if (m >= M) break;
+    const bf16_t* hrow = (const bf16_t*)ep.fin_out + (int64_t)m * ep.fin_ldc;
+    float h[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) load8(hrow + (q * 64 + lane) * 8, h[q]);
+    float ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += h[q][e] * h[q][e];
+    ss = wave_sum(ss);
+    const float rr = 1.0f / sqrtf(ss / 2048.0f + ep.mod_eps);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = (q * 64 + lane) * 8;
+      float s1[8], sh[8], o[8];
+      load8((const bf16_t*)ep.mod_scale1 + n, s1);
+      load8((const bf16_t*)ep.mod_shift + n, sh);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = ((h[q][e] * rr) * s1[e]) + sh[e];
+      store8((bf16_t*)ep.mod_out + (int64_t)m * ep.ld_mod + n, o);
+    }
+  }
+  if (threadIdx.x == 0) sync_depart(pcnt, (uint32_t)pw);
 }
 
 template <int BM, int BN, int WM, int WN, int EK, int NS>
@@ -618,10 +719,12 @@ gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __r
     compute(lds + (kt % NS) * STAGE);
   }
 
-  if constexpr (EK == EK_PARTIAL) {
+  if constexpr (EK == EK_PARTIAL || EK == EK_PARTIAL_FUSED) {
     // fp32 partial tile -> ws slab s: lane holds row (lane & 15) of each 16-row fragment, 4 consecutive
-    // columns 4 (lane >> 4) .. + 3 of each 16-column fragment
+    // columns 4 (lane >> 4) .. + 3 of each 16-column fragment (FUSED: write-through, byte offsets < 4 GiB)
     float* slab = (float*)Cv + (int64_t)s * M * ldc;
+    const __amdgpu_buffer_rsrc_t wsr = rsrc_of(Cv, 0xFFFFFFF0u);
+    (void)wsr;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int m = m0 + wm * TM + i * 16 + frow;
@@ -629,9 +732,17 @@ gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __r
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int n = n0 + wn * TN + j * 16 + 4 * (lane >> 4);
-        if (n < N) *(f32x4*)(slab + (int64_t)m * ldc + n) = acc[i][j];
+        if (n < N) {
+          if constexpr (EK == EK_PARTIAL_FUSED) {
+            const f32x4 v = acc[i][j];
+            st_sc1_b128(wsr, (uint32_t)((((int64_t)s * M + m) * ldc + n) * 4), make_float4(v[0], v[1], v[2], v[3]));
+          } else {
+            *(f32x4*)(slab + (int64_t)m * ldc + n) = acc[i][j];
+          }
+        }
       }
     }
+    if constexpr (EK == EK_PARTIAL_FUSED) sk_fused_finish<BM, BN, NT>(Cv, M, N, S, s, tm, tn, tiles_m, tiles_n, m0, n0, ep);
   } else {
     __syncthreads();  // last fragment reads done before the epilogue reuses the LDS
     gemm_epilogue<TM, TN, FM, FN, EK>(acc, lds, wid, wm, wn, lane, m0, n0, M, N, 0, Cv, ldc, 0, ep);
@@ -2587,11 +2698,33 @@ int launch_sk_direct(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int NS>
+// the split-K finish of a gated residual runs inside the launch (EK_PARTIAL_FUSED) when a counter buffer is set
+// (echo_set_sync_buffer), every workgroup fits on the chip at once and the counters and byte offsets fit
+bool sk_fused_ok(const EchoGemmArgs* a, int tm, int tn, int S) {
+  return g_sync && ek_of(a) == EK_RESID && S > 1 && (int64_t)tm * tn * S <= cu_count_cached() &&
+         SYNC_CNT0 + 2 * ((int64_t)tm * tn + tm) <= g_sync_words &&
+         (int64_t)S * a->M * a->N * 4 < ((int64_t)1 << 32) - 16 &&
+         (int64_t)a->M * a->ldc * 2 < ((int64_t)1 << 32) - 16 && (uintptr_t)a->C % 16 == 0;
+}
+
+template <int BM, int BN, int WM, int WN, int NS, bool FUSE_OK = false>
 int launch_sk(const EchoGemmArgs* a, const Epi& ep, int S, void* ws, hipStream_t s) {
   const int ek = ek_of(a);
   const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;
   const bool mod = ep.mod_out != nullptr;  // caller checked: RESID, N == 2048, partial plan
+  if constexpr (FUSE_OK) {
+    if (sk_fused_ok(a, tm, tn, S)) {  // one launch: the K-slices finish the tiles (and the AdaLN) themselves
+      Epi ef = ep;
+      ef.fin_out = a->C;
+      ef.fin_ldc = a->ldc;
+      ef.sync = g_sync;
+      hipLaunchKernelGGL((gemm_bf16_sk_kernel<BM, BN, WM, WN, EK_PARTIAL_FUSED, NS>), dim3(tm * tn, S),
+                         dim3(64 * WM * WN), 0, s, (const bf16_t*)a->A, a->lda, (const bf16_t*)a->W, a->ldw, ws,
+                         (int64_t)a->N, a->M, a->N, a->K, tm, tn, ef);
+      ECHO_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   if (!mod && !(S > 1 || !sk_direct(BM / WM, BN / WN, ek))) {
     switch (ek) {
       case EK_STORE: return launch_sk_direct<BM, BN, WM, WN, NS, EK_STORE>(a, ep, s);
@@ -2627,12 +2760,12 @@ int launch_sk_cfg(const EchoGemmArgs* a, const Epi& ep, int c, int S, void* ws, 
   switch (c) {
     case 1: return launch_sk<128, 128, 2, 2, 4>(a, ep, S, ws, s);
     case 2: return launch_sk<128, 64, 2, 2, 4>(a, ep, S, ws, s);
-    case 3: return launch_sk<64, 64, 2, 2, 4>(a, ep, S, ws, s);
+    case 3: return launch_sk<64, 64, 2, 2, 4, true>(a, ep, S, ws, s);
     case 4: return launch_sk<160, 64, 2, 2, 4>(a, ep, S, ws, s);
-    case 5: return launch_sk<64, 128, 2, 2, 4>(a, ep, S, ws, s);
-    case 6: return launch_sk<128, 128, 2, 4, 4>(a, ep, S, ws, s);
+    case 5: return launch_sk<64, 128, 2, 2, 4, true>(a, ep, S, ws, s);
+    case 6: return launch_sk<128, 128, 2, 4, 4, true>(a, ep, S, ws, s);
     case 7: return launch_sk<128, 64, 2, 4, 4>(a, ep, S, ws, s);
-    case 8: return launch_sk<64, 64, 2, 4, 4>(a, ep, S, ws, s);
+    case 8: return launch_sk<64, 64, 2, 4, 4, true>(a, ep, S, ws, s);
     case 9: return launch_sk<64, 128, 2, 4, 4>(a, ep, S, ws, s);
     case 10: return launch_sk<160, 128, 2, 2, 4>(a, ep, S, ws, s);
     case 11: return launch_sk<160, 256, 2, 2, 3>(a, ep, S, ws, s);

@@ -175,9 +175,10 @@ def _gemm_args(a, w, c_ptr, ldc, epi, M, N, K, tile):
     return g
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("epi", ["store", "swiglu", "resid", "resid_mod", "headnorm"])
 @pytest.mark.parametrize("cfg,S", [(8, 2), (5, 4), (6, 3), (13, 2)])
-def test_no_store_past_end_splitk_finish(epi, cfg, S):
+def test_no_store_past_end_splitk_finish(epi, cfg, S, fused):
     """The small-M kernel split S ways (fp32 slabs in an exact-size workspace) and gemm_splitk_finish_kernel with
     each fused epilogue at a ragged M (77 rows): output, residual-in-place, the next AdaLN's rows and the
     workspace all stay inside their buffers."""
@@ -219,9 +220,18 @@ def test_no_store_past_end_splitk_finish(epi, cfg, S):
     assert wsb == S * M * N * 4, (wsb, S * M * N * 4)
     wa = Arena(wsb)
     ws = wa.view(torch.uint8, (wsb,))
-    ok(lib().echo_gemm_ws(C.byref(g), ws.data_ptr(), wsb, stream()), "echo_gemm_ws")
+    sa = Arena(4096 * 4)
+    sync = sa.view(torch.int32, (4096,), fill=torch.zeros(4096, dtype=torch.int32, device=DEV))
+    if fused:  # the finish inside the launch (gated residual only; other epilogues keep the finish kernel)
+        ok(lib().echo_set_sync_buffer(sync.data_ptr(), 4096), "echo_set_sync_buffer")
+    try:
+        ok(lib().echo_gemm_ws(C.byref(g), ws.data_ptr(), wsb, stream()), "echo_gemm_ws")
+    finally:
+        lib().echo_set_sync_buffer(None, 0)
     ar.check(f"split-K {epi} output")
     wa.check(f"split-K {epi} workspace")
+    sa.check("in-launch finish counters")
+    assert int(sync.abs().sum()) == 0, "counters not reset"
     if mar is not None:
         mar.check("split-K residual + AdaLN rows")
     assert torch.isfinite(out.float()).all()

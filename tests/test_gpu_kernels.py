@@ -1146,6 +1146,68 @@ def test_gemm_small_m_policy_rows():
     lib = L.load()
     assert lib.echo_set_policy_rows(1, 2) != 0 and lib.echo_set_policy_rows(0, 1) != 0
 
+@pytest.mark.parametrize("M", [77, 160, 480])
+@pytest.mark.parametrize("mod", [True, False])
+def test_gemm_split_finish_in_launch_bitwise(M, mod):
+    """The split-K gated residual (+ the next AdaLN) finished inside the launch (ops.in_launch_sync: write-through
+    slabs, per-tile and per-row-panel arrival counters, the finish kernel's arithmetic) is bitwise the GEMM + finish
+    kernel form, for every fusable small-M config and split count whose grid fits the chip, repeated and
+    graph-replayed; the counter buffer ends zero and no bounded wait gave up."""
+    N, K, eps = 2048, 1024, 1e-5
+    torch.manual_seed(M + mod)
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.03).to(BF)
+    h0 = torch.randn(M, N, device=DEV).to(BF)
+    g = (torch.rand(N, device=DEV) + 0.5).to(BF)
+    sh = (torch.randn(N, device=DEV) * 0.1).to(BF)
+    s1 = (torch.rand(N, device=DEV) + 0.5).to(BF)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    tiles = {3: (64, 64), 5: (64, 128), 6: (128, 128), 8: (64, 64)}
+
+    def run(tile):
+        h = h0.clone()
+        xn = torch.full_like(h, float("nan"))
+        if mod:
+            ops.gemm_resid_norm(a, w, h, g, sh, s1, eps, xn, tile=tile)
+        else:
+            ops.gemm(a, w, out=h, epilogue=L.EPI_RESID, aux=h, gate=g, tile=tile)
+        return h, xn
+
+    buf = ops.new_sync_buffer(DEV)
+    ran = 0
+    for c, (bm, bn) in tiles.items():
+        for S in (2, 3, 4):
+            if -(-M // bm) * (N // bn) * S > cus:
+                continue
+            tile = 100 + 10 * c + S
+            rh, rx = run(tile)
+            with ops.in_launch_sync(buf):
+                for _ in range(2):
+                    fh, fx = run(tile)
+                    torch.cuda.synchronize()
+                    assert torch.equal(fh, rh), (tile, float((fh.float() - rh.float()).abs().max()))
+                    if mod:
+                        assert torch.equal(fx, rx), (tile, float((fx.float() - rx.float()).abs().max()))
+                hg, xg = h0.clone(), torch.empty_like(h0)
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    if mod:
+                        ops.gemm_resid_norm(a, w, hg, g, sh, s1, eps, xg, tile=tile)
+                    else:
+                        ops.gemm(a, w, out=hg, epilogue=L.EPI_RESID, aux=hg, gate=g, tile=tile)
+            for _ in range(2):
+                hg.copy_(h0)
+                gr.replay()
+                torch.cuda.synchronize()
+                assert torch.equal(hg, rh), tile
+                if mod:
+                    assert torch.equal(xg, rx), tile
+            ran += 1
+    assert ran >= 4, ran
+    assert int(buf.abs().sum()) == 0, "counters left non-zero"
+    assert ops.sync_errors(buf) == 0
+
+
 
 @pytest.mark.parametrize("M,K", [(160, 2048), (160, 5888), (480, 5888), (640, 2048), (640, 5888), (1920, 2048),
                                  (333, 5888)])
