@@ -2701,7 +2701,7 @@ int launch_sk_direct(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 // the split-K finish of a gated residual runs inside the launch (EK_PARTIAL_FUSED) when a counter buffer is set
 // (echo_set_sync_buffer), every workgroup fits on the chip at once and the counters and byte offsets fit
 bool sk_fused_ok(const EchoGemmArgs* a, int tm, int tn, int S) {
-  return g_sync && ek_of(a) == EK_RESID && S > 1 && (int64_t)tm * tn * S <= cu_count_cached() &&
+  return g_sync && ek_of(a) == EK_RESID && (S > 1 || a->mod_out) && (int64_t)tm * tn * S <= cu_count_cached() &&
          SYNC_CNT0 + 2 * ((int64_t)tm * tn + tm) <= g_sync_words &&
          (int64_t)S * a->M * a->N * 4 < ((int64_t)1 << 32) - 16 &&
          (int64_t)a->M * a->ldc * 2 < ((int64_t)1 << 32) - 16 && (uintptr_t)a->C % 16 == 0;
@@ -2887,15 +2887,28 @@ extern "C" int echo_set_policy_rows(int32_t num, int32_t den) {
   return 0;
 }
 
+// configs whose launch_sk instantiates the in-launch finish (EK_PARTIAL_FUSED): the residual plans' tiles
+bool sk_fuse_cfg(int c) { return c == 3 || c == 5 || c == 6 || c == 8; }
+
+// workspace of a small-M launch: the split slabs, or — a gated residual + next AdaLN whose plan does not split K
+// but whose grid fits the chip while a counter buffer is set — the one slab of the in-launch finish (the GEMM +
+// modulate pass become one launch)
+int64_t sk_ws_bytes_mod(const EchoGemmArgs* a, int c, int S) {
+  const int64_t need = sk_ws_bytes(a, c, S);
+  if (need > 0 || !a->mod_out || S != 1 || !sk_fuse_cfg(c) || a->N != 2048) return need;
+  const int tm = (a->M + kSk[c].bm - 1) / kSk[c].bm, tn = (a->N + kSk[c].bn - 1) / kSk[c].bn;
+  return sk_fused_ok(a, tm, tn, 1) ? (int64_t)a->M * a->N * 4 : 0;
+}
+
 extern "C" int64_t echo_gemm_ws_bytes(const EchoGemmArgs* a) {
   if (!a || a->M <= 0 || a->N <= 0 || a->K <= 0 || a->K % BK) return 0;
   if (sk_tile(a->tile)) {
     const int c = (a->tile - 100) / 10, S = a->tile % 10;
     if (c < 1 || c > kNumSk || S < 1 || !sk_ok(a)) return 0;
-    return sk_ws_bytes(a, c, S);
+    return sk_ws_bytes_mod(a, c, S);
   }
   int c = 0, S = 1;
-  if (a->tile == 0 && sk_plan(a, true, &c, &S)) return sk_ws_bytes(a, c, S);
+  if (a->tile == 0 && sk_plan(a, true, &c, &S)) return sk_ws_bytes_mod(a, c, S);
   return 0;
 }
 
@@ -2968,7 +2981,7 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
     } else if (a->tile != 0 || !sk_plan(a, ws != nullptr, &c, &S)) {
       c = 0;
     }
-    const int64_t need = c >= 1 && c <= kNumSk && sk_ok(a) ? sk_ws_bytes(a, c, S) : 0;
+    const int64_t need = c >= 1 && c <= kNumSk && sk_ok(a) ? sk_ws_bytes_mod(a, c, S) : 0;
     if (a->dtype == ECHO_BF16 && a->N == 2048 && aligned && need > 0 && a->K / BK >= S && ws &&
         (uintptr_t)ws % 16 == 0 && ws_bytes >= need) {
       Epi em = ep;

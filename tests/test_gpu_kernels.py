@@ -1151,8 +1151,9 @@ def test_gemm_small_m_policy_rows():
 def test_gemm_split_finish_in_launch_bitwise(M, mod):
     """The split-K gated residual (+ the next AdaLN) finished inside the launch (ops.in_launch_sync: write-through
     slabs, per-tile and per-row-panel arrival counters, the finish kernel's arithmetic) is bitwise the GEMM + finish
-    kernel form, for every fusable small-M config and split count whose grid fits the chip, repeated and
-    graph-replayed; the counter buffer ends zero and no bounded wait gave up."""
+    kernel form — and, unsplit with the AdaLN, the direct-epilogue GEMM + modulate pass — for every fusable small-M
+    config and split count whose grid fits the chip, repeated and graph-replayed; the counter buffer ends zero and no
+    bounded wait gave up."""
     N, K, eps = 2048, 1024, 1e-5
     torch.manual_seed(M + mod)
     a = torch.randn(M, K, device=DEV).to(BF)
@@ -1176,7 +1177,7 @@ def test_gemm_split_finish_in_launch_bitwise(M, mod):
     buf = ops.new_sync_buffer(DEV)
     ran = 0
     for c, (bm, bn) in tiles.items():
-        for S in (2, 3, 4):
+        for S in ((1, 2, 3, 4) if mod else (2, 3, 4)):  # S = 1 with the AdaLN: GEMM + modulate pass -> one launch
             if -(-M // bm) * (N // bn) * S > cus:
                 continue
             tile = 100 + 10 * c + S
