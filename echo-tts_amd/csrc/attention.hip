@@ -1660,8 +1660,10 @@ extern "C" int echo_set_sync_buffer(uint32_t* sync, int64_t words) {
   return 0;
 }
 
+extern int g_no_inlaunch_merge;  // echo_gemm_set_diag key 15 (gemm.hip)
+
 extern "C" int32_t echo_attention_merge_in_launch(const EchoAttnArgs* a, int32_t nsplit) {
-  if (!g_sync || !a || nsplit < 2 || nsplit > 16 || a->rows <= 0 || a->heads <= 0 || a->n_q <= 0) return 0;
+  if (!g_sync || g_no_inlaunch_merge || !a || nsplit < 2 || nsplit > 16 || a->rows <= 0 || a->heads <= 0 || a->n_q <= 0) return 0;
   const int64_t items = (int64_t)attn_grid(a, 128);
   // every split of an item must be resident at once: at most one workgroup per CU; counters must fit
   return items * nsplit <= cu_count() && SYNC_CNT0 + 2 * items <= g_sync_words &&

@@ -2700,8 +2700,11 @@ int launch_sk_direct(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 
 // the split-K finish of a gated residual runs inside the launch (EK_PARTIAL_FUSED) when a counter buffer is set
 // (echo_set_sync_buffer), every workgroup fits on the chip at once and the counters and byte offsets fit
+int g_no_fused_finish = 0;  // echo_gemm_set_diag key 14: 1 = never finish split-K inside the launch (A/B)
+int g_no_inlaunch_merge = 0;  // key 15: 1 = split-KV attention never merges inside its launch (A/B; attention.hip)
+
 bool sk_fused_ok(const EchoGemmArgs* a, int tm, int tn, int S) {
-  return g_sync && ek_of(a) == EK_RESID && (S > 1 || a->mod_out) && (int64_t)tm * tn * S <= cu_count_cached() &&
+  return g_sync && !g_no_fused_finish && ek_of(a) == EK_RESID && (S > 1 || a->mod_out) && (int64_t)tm * tn * S <= cu_count_cached() &&
          SYNC_CNT0 + 2 * ((int64_t)tm * tn + tm) <= g_sync_words &&
          (int64_t)S * a->M * a->N * 4 < ((int64_t)1 << 32) - 16 &&
          (int64_t)a->M * a->ldc * 2 < ((int64_t)1 << 32) - 16 && (uintptr_t)a->C % 16 == 0;
@@ -2871,6 +2874,8 @@ extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   else if (key == 11) g_gemm_no_splitk = value != 0;
   else if (key == 12) g_gemm_no_sk = value != 0;
   else if (key == 13) { if (value < 0 || value > 64) return ECHO_EINVAL; g_gemm_group_m = value; }
+  else if (key == 14) g_no_fused_finish = value != 0;
+  else if (key == 15) g_no_inlaunch_merge = value != 0;
   else return ECHO_EINVAL;
   return 0;
 }
