@@ -35,10 +35,12 @@ INIT_SCALE = 0.999  # inference.py:470
 #   C5, 16 x 160-latent blocks: 2 x 8 is 6.4 % slower (M = 3840 per launch is too small to fill the chip).
 STREAM_SPLIT_MIN_TOKENS = int(os.environ.get("ECHO_STREAM_SPLIT_MIN_TOKENS", "0"))
 
-# Split-KV attention of the under-filled launches (B = 1, blockwise blocks) merges its splits inside the split
-# launch (ops.in_launch_sync with a per-plan counter buffer) instead of a separate combine pass: one launch fewer
-# per attention, bitwise the same output. ECHO_INLAUNCH_MERGE=0 turns it off (A/B).
-INLAUNCH_MERGE = os.environ.get("ECHO_INLAUNCH_MERGE", "1") != "0"
+# In-launch hand-offs for the under-filled launches (B = 1, blockwise blocks; ops.in_launch_sync with a per-plan
+# counter buffer): split-KV attention merges its splits inside the split launch, and split-K gated residuals (+ the
+# next AdaLN) finish inside the GEMM launch — fewer launches per layer, bitwise the same output. Measured SLOWER
+# end to end (C2 141.3 -> 134.1, C5 B = 1 68.0 -> 55.4 audio-s/s, profiles/r6_inlaunch_ab.jsonl), so off by
+# default; ECHO_INLAUNCH_MERGE=1 turns it on (A/B).
+INLAUNCH_MERGE = os.environ.get("ECHO_INLAUNCH_MERGE", "0") != "0"
 
 
 @dataclass(frozen=True)
