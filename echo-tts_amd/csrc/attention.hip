@@ -1653,8 +1653,14 @@ extern "C" int echo_attention_set_split(int32_t nsplit) {
 uint32_t* g_sync = nullptr;  // echo_set_sync_buffer: caller-owned counters of in-launch merges (0 words = off)
 int64_t g_sync_words = 0;
 
+// The in-launch hand-offs (the split-KV merge here, the split-K finish in gemm.hip) were measured slower than the
+// kernel boundaries they remove (C5 B = 1 68.0 -> 55.4 audio-s/s), so they exist in the
+// diagnostics build only (ECHO_DIAG=1); the product library refuses a counter buffer.
 extern "C" int echo_set_sync_buffer(uint32_t* sync, int64_t words) {
   if ((sync == nullptr) != (words == 0) || words < 0 || (uintptr_t)sync % 64) return ECHO_EINVAL;
+#ifndef ECHO_DIAG
+  if (sync) return ECHO_EINVAL;
+#endif
   g_sync = sync;
   g_sync_words = words;
   return 0;
@@ -1678,12 +1684,14 @@ extern "C" int echo_attention_split(const EchoAttnArgs* a, int32_t nsplit, void*
   if (nsplit > 16) return ECHO_EINVAL;
   if (!ws || (uintptr_t)ws % 16 || ws_bytes < echo_attention_split_ws_bytes(a, nsplit)) return ECHO_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+#ifdef ECHO_DIAG
   if (echo_attention_merge_in_launch(a, nsplit)) {  // one launch: the splits merge themselves (SP = 2)
     hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 0, 2>), dim3(attn_grid(a, 128) * nsplit), dim3(256), 0, s, *a,
                        (float*)ws, (int)nsplit, g_sync);
     ECHO_LAUNCH_CHECK();
     return 0;
   }
+#endif
   hipLaunchKernelGGL((attn_bf16_kernel<0, 4, 2, 64, 0, 1>), dim3(attn_grid(a, 128) * nsplit), dim3(256), 0, s, *a,
                      (float*)ws, (int)nsplit, (uint32_t*)nullptr);
   ECHO_LAUNCH_CHECK();

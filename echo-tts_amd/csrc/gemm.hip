@@ -2715,6 +2715,7 @@ int launch_sk(const EchoGemmArgs* a, const Epi& ep, int S, void* ws, hipStream_t
   const int ek = ek_of(a);
   const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;
   const bool mod = ep.mod_out != nullptr;  // caller checked: RESID, N == 2048, partial plan
+#ifdef ECHO_DIAG  // measured slower than GEMM + finish kernel: diagnostics build only
   if constexpr (FUSE_OK) {
     if (sk_fused_ok(a, tm, tn, S)) {  // one launch: the K-slices finish the tiles (and the AdaLN) themselves
       Epi ef = ep;
@@ -2728,6 +2729,7 @@ int launch_sk(const EchoGemmArgs* a, const Epi& ep, int S, void* ws, hipStream_t
       return 0;
     }
   }
+#endif
   if (!mod && !(S > 1 || !sk_direct(BM / WM, BN / WN, ek))) {
     switch (ek) {
       case EK_STORE: return launch_sk_direct<BM, BN, WM, WN, NS, EK_STORE>(a, ep, s);

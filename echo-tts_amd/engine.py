@@ -39,7 +39,7 @@ STREAM_SPLIT_MIN_TOKENS = int(os.environ.get("ECHO_STREAM_SPLIT_MIN_TOKENS", "0"
 # counter buffer): split-KV attention merges its splits inside the split launch, and split-K gated residuals (+ the
 # next AdaLN) finish inside the GEMM launch — fewer launches per layer, bitwise the same output. Measured SLOWER
 # end to end (C2 141.3 -> 134.1, C5 B = 1 68.0 -> 55.4 audio-s/s, profiles/r6_inlaunch_ab.jsonl), so off by
-# default; ECHO_INLAUNCH_MERGE=1 turns it on (A/B).
+# default and in the diagnostics build only (ECHO_DIAG=1 library); ECHO_INLAUNCH_MERGE=1 turns it on there (A/B).
 INLAUNCH_MERGE = os.environ.get("ECHO_INLAUNCH_MERGE", "0") != "0"
 
 

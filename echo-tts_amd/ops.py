@@ -223,14 +223,17 @@ def _set_sync(buf: Optional[Tensor]) -> None:
             raise ValueError("in_launch_sync: a contiguous, 64-B aligned int32 device buffer is required")
         rc = lib().echo_set_sync_buffer(buf.data_ptr(), buf.numel())
     if rc:
-        raise RuntimeError(f"echo_set_sync_buffer refused: {L.ERRORS.get(rc, rc)}")
+        raise RuntimeError(f"echo_set_sync_buffer refused: {L.ERRORS.get(rc, rc)} (the in-launch hand-offs "
+                           "measured slower than the kernel boundaries they remove and are in the diagnostics "
+                           "build, ECHO_DIAG=1, only)")
     _SYNC = buf
 
 
 @contextlib.contextmanager
 def in_launch_sync(buf: Optional[Tensor]):
-    """Inside the block, split-KV attention launches whose splits can all be resident merge them inside the
-    launch (one kernel instead of split + combine, bitwise the same output), with `buf`'s counters
+    """Diagnostics build only. Inside the block, split-KV attention launches whose splits can all be resident
+    merge them inside the launch and split-K GEMMs finish inside the launch (one kernel instead of two, bitwise
+    the same output), with `buf`'s counters
     (echo_set_sync_buffer; None = off). The engine's plans run and capture their step loop inside this block
     with their own buffer; restores the previous buffer on exit."""
     prev = _SYNC

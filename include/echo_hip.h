@@ -176,12 +176,16 @@ int echo_attention(const EchoAttnArgs* args, void* stream);
  * Replaces the same reference lines as echo_attention (model.py:237-264, 144-157). */
 int echo_attention_split(const EchoAttnArgs* args, int32_t nsplit, void* ws, int64_t ws_bytes, void* stream);
 int64_t echo_attention_split_ws_bytes(const EchoAttnArgs* args, int32_t nsplit);
-/* In-launch merge (round 6). `sync`: a caller-owned device buffer of `words` uint32 (64-B aligned, zero before
+/* In-launch hand-offs (round 6) — DIAGNOSTICS BUILD (ECHO_DIAG=1) ONLY: measured slower end to end than the
+ * kernel boundaries they remove (profiles/r6_inlaunch_ab.jsonl), so the product library
+ * refuses a non-NULL buffer with ECHO_EINVAL and echo_attention_merge_in_launch answers 0 there.
+ * `sync`: a caller-owned device buffer of `words` uint32 (64-B aligned, zero before
  * its first use, never used by two launches that can run at the same time — e.g. one per captured plan / stream)
  * holding the arrival counters of merges done inside one launch; every such launch leaves it zero again.
  * NULL / 0 (default) = off. While it is set, echo_attention_split merges the splits inside its launch when every
  * split of every item can be resident at once (at most one workgroup per CU) — one kernel instead of the split
- * kernel + combine pass, bitwise the same output. Process-global (like echo_set_policy_rows); a captured graph
+ * kernel + combine pass — and split-K gated-residual GEMMs whose grid fits finish inside their launch (one kernel
+ * instead of GEMM + finish pass); bitwise the same output. Process-global (like echo_set_policy_rows); a captured graph
  * keeps the pointer set when it was captured. Word 0 becomes non-zero if a bounded wait ever gave up (never in a
  * correct run: tests read it). */
 int echo_set_sync_buffer(uint32_t* sync, int64_t words);

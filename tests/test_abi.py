@@ -256,7 +256,9 @@ def test_gemm_small_m_plan_host_policy(lib):
     assert lib.echo_set_sync_buffer(fake + 4, 4096) != 0 and lib.echo_set_sync_buffer(None, 16) != 0
     assert lib.echo_set_sync_buffer(fake, 0) != 0
     assert lib.echo_attention_merge_in_launch(None, 3) == 0
-    assert lib.echo_set_sync_buffer(fake, 4096) == 0  # (its grid / residency rule: test_gpu_kernels.py policy test)
+    # the in-launch hand-offs are in the diagnostics build only: the product library refuses a buffer
+    want = 0 if " diag " in lib.echo_version().decode() else -1
+    assert lib.echo_set_sync_buffer(fake, 4096) == want
     assert lib.echo_set_sync_buffer(None, 0) == 0
 
 

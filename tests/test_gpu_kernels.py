@@ -495,6 +495,9 @@ def test_attention_split_merge_in_launch_bitwise(nsplit, R, n_q, causal):
     counters, the combine's arithmetic per query and 8 columns) is bitwise the split kernel + combine pass; every
     launch leaves the counter buffer zero (the next one starts clean), repeated and graph-replayed launches
     agree, and no bounded wait gave up (word 0)."""
+    if not diag_build():  # measured slower than the kernel boundaries it removes: diagnostics build only
+        assert_refused(lambda: ops.in_launch_sync(ops.new_sync_buffer(DEV)).__enter__())
+        pytest.skip("in-launch hand-offs: diagnostics build (ECHO_DIAG=1) only")
     if causal:
         qkv = torch.randn(R, n_q, 4, 3, 128, device=DEV).to(BF)
         q, gate, segs = qkv[:, :, 0], None, [ops.Segment(qkv[:, :, 1], qkv[:, :, 2], causal=True)]
@@ -529,6 +532,9 @@ def test_attention_split_merge_in_launch_bitwise(nsplit, R, n_q, causal):
 def test_attention_merge_in_launch_policy():
     """The in-launch merge is taken only while a counter buffer is set and only for grids of at most one
     workgroup per CU (every split of an item resident at once); otherwise the two-kernel form runs."""
+    if not diag_build():  # measured slower than the kernel boundaries it removes: diagnostics build only
+        assert_refused(lambda: ops.in_launch_sync(ops.new_sync_buffer(DEV)).__enter__())
+        pytest.skip("in-launch hand-offs: diagnostics build (ECHO_DIAG=1) only")
     qkvg, segs = _small_batch_segments(1, 1, 640, H=16, tl_valid=300)
     buf = ops.new_sync_buffer(DEV)
     cus = torch.cuda.get_device_properties(0).multi_processor_count
@@ -1154,6 +1160,9 @@ def test_gemm_split_finish_in_launch_bitwise(M, mod):
     kernel form — and, unsplit with the AdaLN, the direct-epilogue GEMM + modulate pass — for every fusable small-M
     config and split count whose grid fits the chip, repeated and graph-replayed; the counter buffer ends zero and no
     bounded wait gave up."""
+    if not diag_build():  # measured slower than the kernel boundaries it removes: diagnostics build only
+        assert_refused(lambda: ops.in_launch_sync(ops.new_sync_buffer(DEV)).__enter__())
+        pytest.skip("in-launch hand-offs: diagnostics build (ECHO_DIAG=1) only")
     N, K, eps = 2048, 1024, 1e-5
     torch.manual_seed(M + mod)
     a = torch.randn(M, K, device=DEV).to(BF)
