@@ -768,22 +768,10 @@ __global__ void __launch_bounds__(64 * NW, NW <= 4 ? (KTT == 32 ? 3 : 2) : 1)
 // Measured and removed (round 5 prune; numbers in DESIGN.md §3 / §7): K / V rings of 3 + 2, 3 + 3, 4 + 4 and
 // 2 + 3 slots with counted waits across the barrier; V(t+1)'s DMA between the X and Y bodies; CFG-adjacent
 // and longest-first block orders; the split-KV form of this kernel (2-4 % slower than attn_bf16_kernel's).
-// STG (NW = 8, round 6, diagnostics build): the two wave groups in opposite phases (cdna_hip_programming.md's
-// ping-pong; MI355X_MICROARCH.md "try a stagger"): two barriers per tile, X(t) and Y(t) between them, waves 4-7 one
-// barrier behind, so each SIMD runs one wave's X (softmax VALU || QK) beside the other's Y (PV || row max). With
-// barriers B_k, group 0 runs X(t) in [B_2t, B_2t+1] and Y(t) in [B_2t+1, B_2t+2], group 1 one barrier later.
-// Group 0 issues K(t+2) at the top of its X(t) into the slot K(t) left (last read by group 1's X(t-1), before
-// B_2t) and waits for it at the end of its Y(t) (before B_2t+2, its first reader group 0's X(t+1)); group 1
-// issues V(t+1) at the top of its X(t) into the slot V(t-1) left (last read by group 1's Y(t-1), before B_2t+1)
-// and waits for it at the end of its Y(t) (before B_2t+3, its first reader group 0's Y(t+1)): every piece has two
-// half-tiles of latency, as in the unstaggered kernel. Same bodies, same order: bitwise equal.
-template <int ABL, int NW = 4, int STG = 0>
+template <int ABL, int NW = 4>
 __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgpu_num_vgpr(96)))
     attn_pl_kernel(EchoAttnArgs a_arg) {
-  static_assert(!STG || NW == 8, "stagger: two groups of four waves");
-  // DMA: every wave issues its share of each tile, or (STG) group 0 all of K and group 1 all of V
-  constexpr int DW = STG ? 4 : NW;
-  constexpr int QB = 32 * NW, DPT = 16 / DW, KTT = KT, NK = 2, NV = 2;
+  constexpr int QB = 32 * NW, DPT = 16 / NW, KTT = KT, NK = 2, NV = 2;
   __shared__ __attribute__((aligned(16))) bf16_t lds[(NK + NV) * KT * 128];  // K slots | V slots
 
   using KArgs = const __attribute__((address_space(4))) EchoAttnArgs;
@@ -796,8 +784,6 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
   const int row = Lr % a.rows, head = Lr / a.rows;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wd = STG ? (w & 3) : w;  // index among the waves that issue this ring's DMA
-  const int grp = STG ? (w >> 2) : 0;
   const int h2 = lane >> 5, ql = lane & 31;
   const int q0 = qb * QB;
   const int qc = min(q0 + w * 32 + ql, a.n_q - 1);
@@ -821,10 +807,10 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
     const bf16_t* base = (part ? c.vb : c.kb) + (int64_t)c.t0 * c.ld;
 #pragma unroll
     for (int i = 0; i < DPT; ++i) {
-      const int r = (i * DW + wd) * 4 + dr;
+      const int r = (i * NW + w) * 4 + dr;
       const uint32_t voff = (uint32_t)(min(r, last) * c.ld + ((dp ^ swz(r)) * 8)) * 2u;
       const uint32_t dst = __builtin_amdgcn_readfirstlane(
-          lds_addr_of(lds + (part * NK + slot) * KT * 128 + ((i * DW + wd) * 4) * 128));
+          lds_addr_of(lds + (part * NK + slot) * KT * 128 + ((i * NW + w) * 4) * 128));
       glds16s(base, voff, dst);
     }
   };
@@ -877,12 +863,8 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
 
   pl_zero_o();
   // prologue: K(0), V(0), K(1) — needed before tile 0's loop iteration; scores, mask and max of tile 0
-  const bool kdma = !STG || grp == 0, vdma = !STG || grp == 1;
-  if (ntiles > 0) {
-    if (kdma) dma_part(kc, 0, 0);
-    if (vdma) dma_part(vc, 1, 0);
-  }
-  if (ntiles > 1 && kdma) dma_part(kc, 0, 1);
+  if (ntiles > 0) { dma_part(kc, 0, 0); dma_part(vc, 1, 0); }
+  if (ntiles > 1) dma_part(kc, 0, 1);
   // Q and the prologue DMA in flight together: one wait (hipcc's vmcnt(0) for Q covers the DMA issued after it)
 #pragma unroll
   for (int ds = 0; ds < 8; ++ds) asm volatile("" ::"v"(qf[ds]));
@@ -899,39 +881,6 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
     }
   }
   asm volatile("s_barrier" ::: "memory");  // every wave's K(0) reads are done: slot 0 takes K(NK)
-  if (STG && grp == 1) asm volatile("s_barrier" ::: "memory");  // waves 4-7: one barrier behind from here
-
-  // STG: group 0 issues K(t+2), group 1 V(t+1); a barrier between X(t) and Y(t); the wait at the end of Y(t)
-  auto iter_stg = [&](int t, auto unr) __attribute__((always_inline)) {
-    constexpr int P = decltype(unr)::value;
-    constexpr int KS = 1 - P, VS = P;
-    if (grp == 0) {
-      if (t + 2 < ntiles && !(ABL & 1)) dma_part(kc, 0, P);
-    } else {
-      if (t + 1 < ntiles && !(ABL & 1)) dma_part(vc, 1, 1 - P);
-    }
-    const float msc = m_run == -INFINITY ? 0.f : -m_run * sl2;
-    float ps;
-    if (!wact) {
-      if (t + 1 < ntiles) advance(mc);
-      asm volatile("s_barrier" ::: "memory");
-    } else if (t + 1 < ntiles) {
-      ps = 0.f;
-      if constexpr (!(ABL & 2)) pl_x_cs<P, KS>(qf, ka, sl2, msc, ps);
-      l_run += ps;
-      mask_tile(std::integral_constant<int, 1 - P>{});
-      asm volatile("s_barrier" ::: "memory");
-      float mx = 0.f, ma;
-      if constexpr (!(ABL & 4)) pl_y_cs<P, VS>(va, mx, ma);
-      decide(mx);
-    } else {
-      if constexpr (P == 0) pl_xl_0(sl2, msc, ps); else pl_xl_1(sl2, msc, ps);
-      l_run += ps;
-      asm volatile("s_barrier" ::: "memory");
-      pl_yl_cs<P, VS>(va);
-    }
-    if constexpr (!(ABL & 8)) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  };
 
   auto iter = [&](int t, auto unr) __attribute__((always_inline)) {
     constexpr int P = decltype(unr)::value;  // t & 1: the score buffer of tile t
@@ -960,18 +909,10 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
     if constexpr (!(ABL & 8)) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   };
   if (ABL & 16) ntiles = 0;
-  if constexpr (STG) {
-    for (int t = 0; t < ntiles; t += 2) {
-      iter_stg(t, std::integral_constant<int, 0>{});
-      if (t + 1 >= ntiles) break;
-      iter_stg(t + 1, std::integral_constant<int, 1>{});
-    }
-  } else {
-    for (int t = 0; t < ntiles; t += 2) {
-      iter(t, std::integral_constant<int, 0>{});
-      if (t + 1 >= ntiles) break;
-      iter(t + 1, std::integral_constant<int, 1>{});
-    }
+  for (int t = 0; t < ntiles; t += 2) {
+    iter(t, std::integral_constant<int, 0>{});
+    if (t + 1 >= ntiles) break;
+    iter(t + 1, std::integral_constant<int, 1>{});
   }
 
   // ---- epilogue (attn_bf16_kernel's row layout): normalise, round, transpose through LDS, gate, store
@@ -1023,10 +964,6 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) __attribute__((amdgp
     if (a.gate) attn_gate(v4, g4);
     attn_store_rows(v4, (bf16_t*)a.out + row * a.o_ld_batch + qw * a.o_ld_tok + head * 128, nv, a.o_ld_tok, lane);
   }
-  // STG: group 0's barrier count catches up with group 1's (its epilogue used the K ring, which nothing reads or
-  // fills any more; group 1's uses the V ring after its own last tile)
-  // (the builtin, not an asm block: owned registers are dead here, tools/check_owned_regs.py checks to the last one)
-  if (STG && grp == 0) __builtin_amdgcn_s_barrier();
 }
 
 // ----------------------------------------------------------------------------- one wave per SIMD, 64 rows
@@ -1609,17 +1546,6 @@ int launch_attn_variant(const EchoAttnArgs* a, int cfg, int abl, hipStream_t s) 
       if (cfg == 20) hipLaunchKernelGGL((attn_pl_kernel<0, 8>), g8, dim3(512), 0, s, *a);
       else if (cfg == 21) hipLaunchKernelGGL((attn_pl_kernel<16, 8>), g8, dim3(512), 0, s, *a);
       else hipLaunchKernelGGL((attn_pl_kernel<6, 8>), g8, dim3(512), 0, s, *a);
-      break;
-    }
-    // 8 waves x 32 queries, the two wave groups in opposite phases (round 6, STG): 26 full (bitwise equal to 0),
-    // 27 no tile loop, 28 no X / Y bodies, 29 no loop DMA
-    case 26: case 27: case 28: case 29: {
-      if (any_causal(a)) return ECHO_EINVAL;
-      const dim3 g8(attn_grid(a, 256));
-      if (cfg == 26) hipLaunchKernelGGL((attn_pl_kernel<0, 8, 1>), g8, dim3(512), 0, s, *a);
-      else if (cfg == 27) hipLaunchKernelGGL((attn_pl_kernel<16, 8, 1>), g8, dim3(512), 0, s, *a);
-      else if (cfg == 28) hipLaunchKernelGGL((attn_pl_kernel<6, 8, 1>), g8, dim3(512), 0, s, *a);
-      else hipLaunchKernelGGL((attn_pl_kernel<1, 8, 1>), g8, dim3(512), 0, s, *a);
       break;
     }
     default: return ECHO_EINVAL;
