@@ -2928,11 +2928,12 @@ extern "C" int32_t echo_gemm_planned_tile(const EchoGemmArgs* a, int64_t ws_byte
   switch (r.kind) {
     case RT_SK: return 100 + 10 * r.c + r.S;
     case RT_T320: return 20;
-    case RT_T320_COLSPLIT: return 201;
-    case RT_W13_COLSPLIT: return 202;
-    case RT_ROWSPLIT: return 203;
-    case RT_HN_SPLIT: return 204;
-    case RT_F32: return 205;
+    // 301-305: past the small-M codes (100 + 10 c + S <= 269), so that no label means two launches
+    case RT_T320_COLSPLIT: return 301;
+    case RT_W13_COLSPLIT: return 302;
+    case RT_ROWSPLIT: return 303;
+    case RT_HN_SPLIT: return 304;
+    case RT_F32: return 305;
     default: return r.t;
   }
 }

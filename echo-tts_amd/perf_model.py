@@ -77,8 +77,8 @@ def blockwise_flops(cfg: EchoConfig, block_sizes: Sequence[int], steps_cfg: int,
 
 def planned_tile(a, w, out, epilogue: int, aux=None, head_norm=None) -> int:
     """The launch the library plans for this GEMM (echo_gemm_planned_tile with the workspace the torch op would
-    allocate; codes in include/echo_hip.h): 100 + 10 c + S for the small-M config c split S ways, 201-203 the
-    column / row splits, else the large-tile kernel."""
+    allocate; codes in include/echo_hip.h): 100 + 10 c + S for the small-M config c split S ways, 301-305 the
+    column / row splits, unfused head norm and fp32, else the large-tile kernel."""
     from . import _lib
     lib = _lib.load()
     g = _lib.GemmArgs()

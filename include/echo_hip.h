@@ -104,10 +104,11 @@ int echo_gemm_pick_tile(int32_t M, int32_t N, int32_t K, int32_t batch);
 int64_t echo_gemm_ws_bytes(const EchoGemmArgs* args);
 /* Host-only query: the launch echo_gemm_ws(args, ws, ws_bytes, .) would make (the same host routine decides both;
  * bench.py's per-launch labels): 100 + 10 c + S = the small-M config c with K split S ways; 2..5 the smaller tile
- * configs; 13 the 2-phase 256x256 kernel; 16 the persistent 256x256 kernel; 20 320-row tiles; 201 the 320-row column
- * split (whole rounds of 320-row tile columns, the rest by the auto pick); 202 the W13 column split at 1537-2048 rows
- * (persistent 256x256 kernel + small-M config 13); 203 the row-tail split (256x256 rounds + a smaller-tile tail);
- * 204 store + echo_head_norm_rope (head norm not fused for the shape); 205 fp32; a forced `tile` is returned as is. */
+ * configs; 13 the 2-phase 256x256 kernel; 16 the persistent 256x256 kernel; 20 320-row tiles; 301 the 320-row column
+ * split (whole rounds of 320-row tile columns, the rest by the auto pick); 302 the W13 column split at 1537-2048 rows
+ * (persistent 256x256 kernel + small-M config 13); 303 the row-tail split (256x256 rounds + a smaller-tile tail);
+ * 304 store + echo_head_norm_rope (head norm not fused for the shape); 305 fp32 (round 6: 301-305, past the small-M
+ * codes, which reach 269); a forced `tile` is returned as is. */
 int32_t echo_gemm_planned_tile(const EchoGemmArgs* args, int64_t ws_bytes);
 int echo_gemm_ws(const EchoGemmArgs* args, void* ws, int64_t ws_bytes, void* stream);
 
