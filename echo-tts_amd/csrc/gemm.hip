@@ -42,6 +42,7 @@ struct Epi {
   void* mod_out; int64_t ld_mod; const void* mod_shift; const void* mod_scale1; float mod_eps;
   // EK_PARTIAL_FUSED (the split-K finish inside the launch): the output, its row stride, the counter buffer
   void* fin_out; int64_t fin_ldc; uint32_t* sync;
+  int abl;  // small-M kernel timing ablations (diagnostics build, echo_gemm_set_diag key 16; results wrong)
 };
 
 // Element offset added to A for the K-slice starting at k0 in conv mode (0 otherwise): tap
@@ -708,16 +709,24 @@ gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __r
   // ring: slots hold K-tiles kt mod NS; at tile kt wait for it (the up to NS - 2 younger tiles stay in
   // flight), barrier (tile kt visible; every wave is done reading tile kt - 1's slot), then refill that
   // slot with tile kt + NS - 1 and compute tile kt
+  // ECHO_DIAG timing ablations (results wrong): 1 no MFMA / fragment reads, 2 no DMA in the loop, 4 no epilogue,
+  // 8 no DMA at all
+#ifdef ECHO_DIAG
+  const int abl = ep.abl;
+#else
+  constexpr int abl = 0;
+#endif
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
-    if (p < nk) stage(p, p);
+    if (p < nk && !(abl & 8)) stage(p, p);
   for (int kt = 0; kt < nk; ++kt) {
     vm_wait_stages<DOPS>(min(NS - 2, nk - 1 - kt));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + NS - 1 < nk) stage(kt + NS - 1, (kt + NS - 1) % NS);
-    compute(lds + (kt % NS) * STAGE);
+    if (kt + NS - 1 < nk && !(abl & 10)) stage(kt + NS - 1, (kt + NS - 1) % NS);
+    if (!(abl & 1)) compute(lds + (kt % NS) * STAGE);
   }
+  if (abl & 4) return;
 
   if constexpr (EK == EK_PARTIAL || EK == EK_PARTIAL_FUSED) {
     // fp32 partial tile -> ws slab s: lane holds row (lane & 15) of each 16-row fragment, 4 consecutive
@@ -2700,6 +2709,7 @@ int launch_sk_direct(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
 
 // the split-K finish of a gated residual runs inside the launch (EK_PARTIAL_FUSED) when a counter buffer is set
 // (echo_set_sync_buffer), every workgroup fits on the chip at once and the counters and byte offsets fit
+int g_sk_abl = 0;  // key 16 (diagnostics build): small-M kernel timing ablations (Epi::abl)
 int g_no_fused_finish = 0;  // echo_gemm_set_diag key 14: 1 = never finish split-K inside the launch (A/B)
 int g_no_inlaunch_merge = 0;  // key 15: 1 = split-KV attention never merges inside its launch (A/B; attention.hip)
 
@@ -2878,6 +2888,9 @@ extern "C" int echo_gemm_set_diag(int32_t key, int32_t value) {
   else if (key == 13) { if (value < 0 || value > 64) return ECHO_EINVAL; g_gemm_group_m = value; }
   else if (key == 14) g_no_fused_finish = value != 0;
   else if (key == 15) g_no_inlaunch_merge = value != 0;
+#ifdef ECHO_DIAG
+  else if (key == 16) g_sk_abl = value;
+#endif
   else return ECHO_EINVAL;
   return 0;
 }
@@ -2969,6 +2982,9 @@ extern "C" int echo_gemm_ws(const EchoGemmArgs* a, void* ws, int64_t ws_bytes, v
          a->hn_w, a->hn_w_stride, a->hn_rope, a->hn_heads, a->hn_nblk, a->hn_rope_heads, a->hn_seq_len,
          a->hn_pos0, a->hn_pos_mult, a->hn_eps, 0, a->act_alpha, a->conv_c, a->conv_taps, a->conv_dil,
          nullptr, 0, nullptr, nullptr, 0.f};
+#ifdef ECHO_DIAG
+  ep.abl = g_sk_abl;
+#endif
   if (a->mod_out) {
     // residual + the next AdaLN: fused into the finish kernel when the small-M plan has one (K split or
     // no direct epilogue) and a row is one finish workgroup (N == 2048); else the GEMM, then
