@@ -660,12 +660,14 @@ gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __r
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // SADDR-form DMA of K-tile kb + kt into ring slot `slot` (32-bit offsets: the host checks the extents)
-  auto stage = [&](int kt, int slot) __attribute__((always_inline)) {
+  // SADDR-form DMA of K-tile kb + kt into ring slot `slot` (32-bit offsets: the host checks the extents);
+  // part 0 = the A pieces, 1 = the W pieces, 2 = both
+  auto stage = [&](int kt, int slot, int part = 2) __attribute__((always_inline)) {
     const int k0 = (kb + kt) * BK;
     const bf16_t* abase = A + k0;
     const bf16_t* wbase = W + k0;
     bf16_t* dst = lds + slot * STAGE;
+    if (part != 1) {
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int rb = ((i * NW + wid) * 8) % BM;
@@ -674,6 +676,8 @@ gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __r
       const uint32_t off = (uint32_t)(((int64_t)min(m0 + row, M - 1) * lda + gc * 8) * 2);
       glds16s(abase, off, __builtin_amdgcn_readfirstlane(lds_addr_of(dst + rb * BK)));
     }
+    }
+    if (part == 0) return;
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       const int rb = ((i * NW + wid) * 8) % BN;
@@ -686,7 +690,11 @@ gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __r
 
   const int frow = lane & 15;
   const int fsw = frow >> 1;
-  auto compute = [&](const bf16_t* As) __attribute__((always_inline)) {
+  // snext >= 0: the DMA of K-tile snext is issued inside the compute, its A pieces after the first half's fragment
+  // reads and its W pieces after the second half's, under their LDS latency and beside the other wave's MFMAs
+  // (issued as one block between the barrier and the compute, each wave's pieces delayed its first fragment reads:
+  // profiles/r6_sk_dma_split.txt)
+  auto compute = [&](const bf16_t* As, int snext = -1, int sslot = 0) __attribute__((always_inline)) {
     const bf16_t* Bs = As + BM * BK;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -696,6 +704,7 @@ gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __r
       for (int i = 0; i < FM; ++i) xf[i] = *(const bf16x8*)(As + (wm * TM + i * 16 + frow) * BK + ph);
 #pragma unroll
       for (int j = 0; j < FN; ++j) wf[j] = *(const bf16x8*)(Bs + (wn * TN + j * 16 + frow) * BK + ph);
+      if (snext >= 0) stage(snext, sslot, ks);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -723,8 +732,14 @@ gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __r
     vm_wait_stages<DOPS>(min(NS - 2, nk - 1 - kt));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + NS - 1 < nk && !(abl & 10)) stage(kt + NS - 1, (kt + NS - 1) % NS);
-    if (!(abl & 1)) compute(lds + (kt % NS) * STAGE);
+    const bool more = kt + NS - 1 < nk && !(abl & 10);
+    if (!(abl & 32)) {  // the next K-tile's DMA issued inside the compute (round 6: 4-12 % faster at B = 1 shapes)
+      if (!(abl & 1)) compute(lds + (kt % NS) * STAGE, more ? kt + NS - 1 : -1, (kt + NS - 1) % NS);
+      else if (more) stage(kt + NS - 1, (kt + NS - 1) % NS);
+    } else {  // diag A/B (bit 32): the round-5 order, all of it between the barrier and the compute
+      if (more) stage(kt + NS - 1, (kt + NS - 1) % NS);
+      if (!(abl & 1)) compute(lds + (kt % NS) * STAGE);
+    }
   }
   if (abl & 4) return;
 

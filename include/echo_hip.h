@@ -137,7 +137,8 @@ int echo_set_policy_rows(int32_t num, int32_t den);
  * key 13: group-M height of the persistent 256x256 and 320-row kernels' tile order (0 = 4; 1..64; bitwise-equal).
  * key 14 / 15: 1 = no in-launch split-K finish / split-KV merge (A/B of echo_set_sync_buffer's hand-offs; no effect in
  * the product library, which has none); key 16 (diagnostics build only, refused here): timing ablations of the
- * small-M kernel (bits: 1 no MFMA, 2 no DMA in the K loop, 4 no epilogue, 8 no DMA at all; results wrong).
+ * small-M kernel (bits: 1 no MFMA, 2 no DMA in the K loop, 4 no epilogue, 8 no DMA at all; results wrong; 32 the
+ * round-5 DMA issue order, results right).
  * `tile` 100 + 10*C + S (C = small-M config 1..16, S = split 1..9) forces a small-M launch (tools/bench_gemm.py).
  * The timing-ablation tiles 7-12 and 15 (results wrong) exist in the diagnostics build (ECHO_DIAG=1) only. */
 int echo_gemm_set_diag(int32_t key, int32_t value);

@@ -1,6 +1,8 @@
 """Timing ablations of the small-M GEMM kernel (gemm_bf16_sk_kernel) at the B = 1 decoder shapes, diagnostics build
 only (echo_gemm_set_diag key 16; results wrong): the auto plan with 1 no MFMA / fragment reads, 2 no DMA in the K loop,
-3 neither (loop skeleton: waits + barriers), 4 no epilogue, 8 no DMA at all (prologue included), 15 empty launch.
+3 neither (loop skeleton: waits + barriers), 4 no epilogue, 8 no DMA at all (prologue included), 15 empty launch,
+32 the round-5 order of the next K-tile's DMA (one block before the compute; results right). SK_ABLS=0,32,... picks
+the list.
 Launches replayed from a graph, weights rotated over 8 copies (tools/sweep_sk_depth.py's timing).
 
     python tools/sk_ablate.py
@@ -21,7 +23,7 @@ DEV = "cuda"
 BF = torch.bfloat16
 SHAPES = [("w13", 480, 11776, 2048, "swiglu"), ("qkvg", 480, 8192, 2048, "headnorm"), ("wo", 480, 2048, 2048, "resid"),
           ("w2", 480, 2048, 5888, "resid"), ("w13", 160, 11776, 2048, "swiglu"), ("w2", 1920, 2048, 5888, "resid")]
-ABLS = [0, 1, 2, 3, 4, 8, 9, 15]
+ABLS = [int(v) for v in os.environ.get("SK_ABLS", "0,1,2,3,4,8,9,15").split(",")]
 
 
 def main():
