@@ -733,7 +733,9 @@ gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __r
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const bool more = kt + NS - 1 < nk && !(abl & 10);
-    if (!(abl & 32)) {  // the next K-tile's DMA issued inside the compute (round 6: 4-12 % faster at B = 1 shapes)
+    // 8-wave configs: the next K-tile's DMA issued inside the compute (round 6: 5-9 % faster at the B = 1 shapes);
+    // with one wave per SIMD nothing runs beside the issue, and the 4-wave configs stay 9 % faster without it
+    if (NW >= 8 && !(abl & 32)) {
       if (!(abl & 1)) compute(lds + (kt % NS) * STAGE, more ? kt + NS - 1 : -1, (kt + NS - 1) % NS);
       else if (more) stage(kt + NS - 1, (kt + NS - 1) % NS);
     } else {  // diag A/B (bit 32): the round-5 order, all of it between the barrier and the compute
