@@ -22,7 +22,8 @@ from tools.sweep_sk_depth import timed  # noqa: E402
 DEV = "cuda"
 BF = torch.bfloat16
 SHAPES = [("w13", 480, 11776, 2048, "swiglu"), ("qkvg", 480, 8192, 2048, "headnorm"), ("wo", 480, 2048, 2048, "resid"),
-          ("w2", 480, 2048, 5888, "resid"), ("w13", 160, 11776, 2048, "swiglu"), ("w2", 1920, 2048, 5888, "resid")]
+          ("w2", 480, 2048, 5888, "resid"), ("w13", 160, 11776, 2048, "swiglu"), ("w2", 1920, 2048, 5888, "resid"),
+          ("wo", 1920, 2048, 2048, "resid"), ("qkvg", 160, 8192, 2048, "headnorm"), ("qkvg", 640, 8192, 2048, "headnorm")]
 ABLS = [int(v) for v in os.environ.get("SK_ABLS", "0,1,2,3,4,8,9,15").split(",")]
 
 
