@@ -157,28 +157,28 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
   const int nbase = (swiglu ? n0 / 2 : n0) + wn * TNo;
   if constexpr (EK == EK_HEADNORM) {
     // q/k RMSNorm + RoPE of echo_head_norm_rope fused after the store rounding. A 128-column
-    // head is either one wave's staged tile (TN == 128) or spans the tiles of waves (wm, 2p) and
-    // (wm, 2p+1) (TN == 64; each wave of the pair then takes half of the pair's rows). 16 lanes
-    // per row, 8 consecutive columns per lane and the same xor-butterfly sum as
-    // head_norm_rope_kernel, so results are bitwise equal.
-    static_assert((TN == 64 || TN == 128) && TM % 8 == 0, "HEADNORM epilogue: 64- or 128-column wave tiles");
-    constexpr bool PAIR = TN == 64;
-    constexpr int PR = PAIR ? TM / 2 : 0;  // rows of the pair's tile taken by the second wave
+    // head is one wave's staged tile (TN == 128) or spans the tiles of the G = 128 / TN waves (wm, G p .. G p + G - 1)
+    // (TN == 64 / 32; each wave of the group then takes 1 / G of the group's rows). 16 lanes per row, 8 consecutive
+    // columns per lane and the same xor-butterfly sum as head_norm_rope_kernel, so results are bitwise equal.
+    static_assert((TN == 32 || TN == 64 || TN == 128) && TM % (128 / TN * 4) == 0,
+                  "HEADNORM epilogue: 32-, 64- or 128-column wave tiles");
+    constexpr int G = 128 / TN;
+    constexpr int PR = TM / G;   // rows of the group's tile taken by each wave
     constexpr int CHS = TN / 8;  // 16-B chunks per staged row
-    if (PAIR) __syncthreads();   // the partner wave's staged tile is complete
-    const int hcol = n0 + (PAIR ? (wn & ~1) : wn) * TN;  // first column of this wave's head
+    if (G > 1) __syncthreads();  // the partner waves' staged tiles are complete
+    const int hcol = n0 + (wn & ~(G - 1)) * TN;  // first column of this wave's head
     const int hidx = hcol >> 7;
     const int blk = hidx / ep.hn_heads, h = hidx - blk * ep.hn_heads;
     const bool norm = blk < ep.hn_nblk;
     const bool rope = norm && h < ep.hn_rope_heads;
     const int ch = lane & 15, rq = lane >> 4;
-    const int c = PAIR ? (ch & 7) : ch;
-    const bf16_t* src = lds + (PAIR ? (wid & ~1) + (ch >> 3) : wid) * (TM * TN);
+    const int c = ch & (CHS - 1);
+    const bf16_t* src = lds + ((wid & ~(G - 1)) + ch / CHS) * (TM * TN);
     float wv[8];
     if (norm) load8((const bf16_t*)ep.hn_w + blk * ep.hn_w_stride + h * 128 + ch * 8, wv);
     bf16_t* Cp = (bf16_t*)Cv + z * sC + hcol + ch * 8;
     if (hcol >= N) return;
-    constexpr int NR = (PAIR ? TM / 2 : TM) / 4;  // 4-row iterations per wave
+    constexpr int NR = PR / 4;  // 4-row iterations per wave
     // Batched: the LDS reads, RoPE table loads, sums, butterflies and reciprocal square roots of
     // HB row iterations are issued together (independent chains interleave) instead of one
     // row iteration's serial chain at a time; per element the same operations in the same order.
@@ -187,7 +187,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
       float v[HB][8];
 #pragma unroll
       for (int b = 0; b < HB; ++b) {
-        const int row = (wn & 1) * PR + (it0 + b) * 4 + rq;
+        const int row = (wn & (G - 1)) * PR + (it0 + b) * 4 + rq;
         load8(src + row * TN + ((c ^ (row & (CHS - 1))) * 8), v[b]);
       }
       if (norm) {
@@ -195,7 +195,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
         if (rope) {
 #pragma unroll
           for (int b = 0; b < HB; ++b) {
-            const int m = m0 + wm * TM + (wn & 1) * PR + (it0 + b) * 4 + rq;
+            const int m = m0 + wm * TM + (wn & (G - 1)) * PR + (it0 + b) * 4 + rq;
             const int pos = ep.hn_pos0 + ep.hn_pos_mult * (min(m, M - 1) % ep.hn_seq_len);
             const float4* cp = (const float4*)(ep.hn_rope + ((int64_t)pos * 64 + ch * 4) * 2);
             cs[b][0] = cp[0];
@@ -236,7 +236,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[FM][FN], bf16_t* lds,
       }
 #pragma unroll
       for (int b = 0; b < HB; ++b) {
-        const int m = m0 + wm * TM + (wn & 1) * PR + (it0 + b) * 4 + rq;
+        const int m = m0 + wm * TM + (wn & (G - 1)) * PR + (it0 + b) * 4 + rq;
         if (m < M) store8(Cp + (int64_t)m * ldc, v[b]);
       }
     }
@@ -2627,11 +2627,12 @@ int sk_occ(int c) { return (160 * 1024) / ((kSk[c].bm + kSk[c].bn) * BK * 2 * kS
 
 // the fused epilogue straight from the unit's registers is expressible for this wave tile (gemm_epilogue's
 // row-chunk loop must divide the wave's rows); otherwise the launch goes through the finish kernel
-constexpr bool sk_direct(int tm, int tn, int ek) {
+constexpr bool sk_direct(int tm, int tn, int ek, int wn) {
   // SwiGLU pairs the w1 / w3 16-column blocks inside a wave: its tile needs whole pairs (tn % 32 == 0);
-  // head norm: a 128-column head in one wave's tile or in a pair of waves' 64-column tiles
+  // head norm: a 128-column head in one wave's tile or in the 64- / 32-column tiles of 2 / 4 waves of one row of the
+  // workgroup's waves (wn % (128 / tn) == 0: the head never spans workgroups)
   return ek == EK_SWIGLU     ? (tn % 32 == 0 && tm % (64 / (tn / 16)) == 0)
-         : ek == EK_HEADNORM ? ((tn == 64 || tn == 128) && tm % 8 == 0)
+         : ek == EK_HEADNORM ? ((tn == 32 || tn == 64 || tn == 128) && tm % (128 / tn * 4) == 0 && wn % (128 / tn) == 0)
                              : (ek == EK_STORE || ek == EK_RESID) && tm % (64 / (tn / 8)) == 0;
 }
 
@@ -2650,7 +2651,7 @@ bool sk_ok(const EchoGemmArgs* a) {
 
 bool sk_partial(int c, int S, int ek) {
   const int tm = kSk[c].bm / kSk[c].wm, tn = kSk[c].bn / kSk[c].wn;
-  return S > 1 || !sk_direct(tm, tn, ek);
+  return S > 1 || !sk_direct(tm, tn, ek, kSk[c].wn);
 }
 
 int64_t sk_ws_bytes(const EchoGemmArgs* a, int c, int S) {
@@ -2694,7 +2695,10 @@ bool sk_plan(const EchoGemmArgs* a, bool allow_split, int* cfg, int* split) {
     else if (Mp > 2048 && Mp <= 3072) c = 15;
     else return false;
   } else if (ek == EK_HEADNORM && a->N >= 4096 && Mp <= 768) {
-    c = Mp <= 256 ? 5 : Mp <= 512 ? 1 : 10;
+    // round 6: the 8-wave configs now fuse the head norm over four waves' 32-column tiles (gemm_epilogue):
+    // 160 / 480 / 640 rows 18.4 -> 17.1 (9), 27.7 -> 23.7 (6), 32.9 -> 28.4 us (16), bitwise equal
+    // (profiles/r6_qkvg_8wave.txt; the 4-wave configs 5 / 1 / 10 before)
+    c = Mp <= 256 ? 9 : Mp <= 512 ? 6 : 16;
   } else if (ek == EK_SWIGLU && a->N >= 8192 && Mp <= 768) {
     c = Mp <= 256 ? 6 : 13;  // 480 / 640 rows: 39.1 -> 35.4 / 38.1 -> 36.9 us (profiles/r4_sk4_sweep.txt)
   } else {
@@ -2712,7 +2716,7 @@ bool sk_plan(const EchoGemmArgs* a, bool allow_split, int* cfg, int* split) {
 template <int BM, int BN, int WM, int WN, int NS, int EK>
 int launch_sk_direct(const EchoGemmArgs* a, const Epi& ep, hipStream_t s) {
   constexpr int TM = BM / WM, TN = BN / WN;
-  if constexpr (sk_direct(TM, TN, EK)) {
+  if constexpr (sk_direct(TM, TN, EK, WN)) {
     const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;
     hipLaunchKernelGGL((gemm_bf16_sk_kernel<BM, BN, WM, WN, EK, NS>), dim3(tm * tn, 1), dim3(64 * WM * WN), 0, s,
                        (const bf16_t*)a->A, a->lda, (const bf16_t*)a->W, a->ldw, a->C, a->ldc, a->M, a->N, a->K, tm,
@@ -2757,7 +2761,7 @@ int launch_sk(const EchoGemmArgs* a, const Epi& ep, int S, void* ws, hipStream_t
     }
   }
 #endif
-  if (!mod && !(S > 1 || !sk_direct(BM / WM, BN / WN, ek))) {
+  if (!mod && !(S > 1 || !sk_direct(BM / WM, BN / WN, ek, WN))) {
     switch (ek) {
       case EK_STORE: return launch_sk_direct<BM, BN, WM, WN, NS, EK_STORE>(a, ep, s);
       case EK_SWIGLU: return launch_sk_direct<BM, BN, WM, WN, NS, EK_SWIGLU>(a, ep, s);

@@ -8,7 +8,7 @@ unsplit configs are checked bitwise against the auto plan's unsplit result; spli
 
     python tools/sweep_sk_depth.py [1920|big] [shape ...]   shapes: w13 qkvg wo w2 (default all); 1920: the C2 CFG rows;
     big: 480 / 640 rows against the large-tile configs; large: the C3 and blockwise B = 16 row counts;
-    gm: the auto plan at each group-M height of the persistent tile orders
+    gm: the auto plan at each group-M height of the persistent tile orders; r6: QKVG on the 8-wave configs
 """
 import os
 import sys
@@ -83,6 +83,10 @@ SHAPES_GM = {  # auto plan vs the group-M height of the persistent 256x256 / 320
     "wo": (2048, 2048, "resid", {30720: [], 10240: [], 7680: []}),
     "w2": (2048, 5888, "resid", {30720: [], 10240: [], 7680: []}),
 }
+SHAPES_R6 = {  # round 6: QKVG on the 8-wave configs (head norm over four waves' 32-column tiles)
+    "qkvg": (8192, 2048, "headnorm", {480: [111, 161, 191, 251, 261], 160: [151, 191, 161, 261],
+                                      640: [201, 161, 191, 251, 261], 1920: [161, 251, 261]}),
+}
 SHAPES_BIG = {  # the small-M row counts against the large-tile configs
     "w13": (11776, 2048, "swiglu", {480: BIG, 640: BIG}),
     "qkvg": (8192, 2048, "headnorm", {480: BIG, 640: BIG}),
@@ -98,8 +102,8 @@ def main():
     args = [v for v in args if v != "--fresh"]
     table = SHAPES
     gm_mode = bool(args) and args[0] == "gm"
-    if args and args[0] in ("1920", "big", "large", "gm"):
-        table = {"1920": SHAPES_1920, "big": SHAPES_BIG, "large": SHAPES_LARGE, "gm": SHAPES_GM}[args[0]]
+    if args and args[0] in ("1920", "big", "large", "gm", "r6"):
+        table = {"1920": SHAPES_1920, "big": SHAPES_BIG, "large": SHAPES_LARGE, "gm": SHAPES_GM, "r6": SHAPES_R6}[args[0]]
         args = args[1:]
     names = args or list(table)
     H = 16
