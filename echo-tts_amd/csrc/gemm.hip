@@ -2686,10 +2686,12 @@ bool sk_plan(const EchoGemmArgs* a, bool allow_split, int* cfg, int* split) {
     // (M <= 256, K 5888: config 3 at S = 4 measured 16.6 -> 15.9 us in isolation, replayed from a graph with the
     // activations L2-resident, but 19.0 -> 21.0 us with its finish inside the sampler, where the activations were
     // just written: 64x64 tiles read them from the fabric twice as often; profiles/r5_sk_depth_sweep.txt)
+    // (round 6, with the 8-wave configs' in-compute DMA: Wo at 640 rows config 3 -> 9, 16.2 -> 14.2 us; at 1920 rows
+    // the 128x64 two-stage tile -> config 6, 23.3 -> 20.9 us; profiles/r6_wo_8wave.txt)
     if (Mp <= 256) { c = longk ? 5 : 8; S = longk ? 4 : 2; }
     else if (Mp <= 512) { c = longk ? 6 : 8; S = longk ? 4 : 1; }
-    else if (Mp <= 768) { c = longk ? 6 : 3; S = longk ? 3 : 1; }
-    else if (Mp <= 2048 && longk) c = 6;
+    else if (Mp <= 768) { c = longk ? 6 : 9; S = longk ? 3 : 1; }
+    else if (Mp <= 2048) c = 6;
     // the blockwise B = 16 plain step (M = 2560: 256 tiles of 160x128 = one round): 37.9 -> 31.3 us (Wo),
     // 85.6 -> 73.3 (W2) (profiles/r4_sk5_sweep.txt; hipBLASLt's plain store 26.7 / 58.5)
     else if (Mp > 2048 && Mp <= 3072) c = 15;

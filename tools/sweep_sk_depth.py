@@ -83,9 +83,13 @@ SHAPES_GM = {  # auto plan vs the group-M height of the persistent 256x256 / 320
     "wo": (2048, 2048, "resid", {30720: [], 10240: [], 7680: []}),
     "w2": (2048, 5888, "resid", {30720: [], 10240: [], 7680: []}),
 }
-SHAPES_R6 = {  # round 6: QKVG on the 8-wave configs (head norm over four waves' 32-column tiles)
+SHAPES_R6 = {  # round 6: QKVG on the 8-wave configs (head norm over four waves' 32-column tiles); Wo / W2 on the
+    # 8-wave configs now that they issue the next tile's DMA inside the compute
     "qkvg": (8192, 2048, "headnorm", {480: [111, 161, 191, 251, 261], 160: [151, 191, 161, 261],
                                       640: [201, 161, 191, 251, 261], 1920: [161, 251, 261]}),
+    "wo": (2048, 2048, "resid", {640: [131, 181, 161, 171, 191, 182], 1920: [4, 161, 171, 191, 162, 172],
+                                 480: [181, 161, 171, 191, 182]}),
+    "w2": (2048, 5888, "resid", {640: [163, 162, 164, 173, 193], 1920: [161, 171, 162, 172]}),
 }
 SHAPES_BIG = {  # the small-M row counts against the large-tile configs
     "w13": (11776, 2048, "swiglu", {480: BIG, 640: BIG}),
