@@ -2688,7 +2688,7 @@ bool sk_plan(const EchoGemmArgs* a, bool allow_split, int* cfg, int* split) {
     // just written: 64x64 tiles read them from the fabric twice as often; profiles/r5_sk_depth_sweep.txt)
     // (round 6, with the 8-wave configs' in-compute DMA: Wo at 640 rows config 3 -> 9, 16.2 -> 14.2 us; at 1920 rows
     // the 128x64 two-stage tile -> config 6, 23.3 -> 20.9 us; profiles/r6_wo_8wave.txt)
-    if (Mp <= 256) { c = longk ? 5 : 8; S = longk ? 4 : 2; }
+    if (Mp <= 256) { c = longk ? 9 : 8; S = longk ? 4 : 2; }  // W2 at 160 rows: 5 -> 9 (8 waves), 16.8 -> 15.0 us
     else if (Mp <= 512) { c = longk ? 6 : 8; S = longk ? 4 : 1; }
     else if (Mp <= 768) { c = longk ? 6 : 9; S = longk ? 3 : 1; }
     else if (Mp <= 2048) c = 6;

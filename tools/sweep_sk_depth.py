@@ -89,7 +89,9 @@ SHAPES_R6 = {  # round 6: QKVG on the 8-wave configs (head norm over four waves'
                                       640: [201, 161, 191, 251, 261], 1920: [161, 251, 261]}),
     "wo": (2048, 2048, "resid", {640: [131, 181, 161, 171, 191, 182], 1920: [4, 161, 171, 191, 162, 172],
                                  480: [181, 161, 171, 191, 182]}),
-    "w2": (2048, 5888, "resid", {640: [163, 162, 164, 173, 193], 1920: [161, 171, 162, 172]}),
+    "w2": (2048, 5888, "resid", {640: [163, 162, 164, 173, 193], 1920: [161, 171, 162, 172],
+                                 160: [154, 194, 193, 195, 184, 164]}),
+    "wo160": (2048, 2048, "resid", {160: [182, 192, 183, 193, 162]}),
 }
 SHAPES_BIG = {  # the small-M row counts against the large-tile configs
     "w13": (11776, 2048, "swiglu", {480: BIG, 640: BIG}),
