@@ -92,6 +92,8 @@ SHAPES_R6 = {  # round 6: QKVG on the 8-wave configs (head norm over four waves'
     "w2": (2048, 5888, "resid", {640: [163, 162, 164, 173, 193], 1920: [161, 171, 162, 172],
                                  160: [154, 194, 193, 195, 184, 164]}),
     "wo160": (2048, 2048, "resid", {160: [182, 192, 183, 193, 162]}),
+    "w13c2": (11776, 2048, "swiglu", {1920: [16, 231, 161, 251, 261]}),
+    "qkvgc2": (8192, 2048, "headnorm", {1920: [13, 231, 161, 251]}),
 }
 SHAPES_BIG = {  # the small-M row counts against the large-tile configs
     "w13": (11776, 2048, "swiglu", {480: BIG, 640: BIG}),
