@@ -93,6 +93,8 @@ SHAPES_R6 = {  # round 6: QKVG on the 8-wave configs (head norm over four waves'
                                  160: [154, 194, 193, 195, 184, 164]}),
     "wo160": (2048, 2048, "resid", {160: [182, 192, 183, 193, 162]}),
     "w13c2": (11776, 2048, "swiglu", {1920: [16, 231, 161, 251, 261]}),
+    "w2s": (2048, 5888, "resid", {480: [164, 163, 165, 166, 162], 160: [194, 193, 195, 196, 192],
+                                  640: [163, 164, 165, 162]}),
     "w13b16": (11776, 2048, "swiglu", {2560: [16, 231, 251, 261], 7680: [20, 231, 251]}),
     "qkvgb16": (8192, 2048, "headnorm", {2560: [20, 161, 251, 261], 7680: [20, 251]}),
     "wob16": (2048, 2048, "resid", {2560: [251, 261, 161], 7680: [16, 251, 261]}),
