@@ -246,6 +246,30 @@ def test_no_store_past_end_splitk_finish(epi, cfg, S, fused):
     assert torch.isfinite(out.float()).all()
 
 
+@pytest.mark.parametrize("cfg", [1, 5, 6, 9, 10, 13, 15, 16])
+def test_no_store_past_end_headnorm_direct(cfg):
+    """The small-M kernel unsplit with the fused q/k norm + RoPE epilogue straight from registers (a head in one wave,
+    in a pair of waves' 64-column tiles or, round 6, in four waves' 32-column tiles) at a ragged M (77 rows), into an
+    output whose rows have a 64-column gap after the 512 columns: the head stores stay inside their rows and rows."""
+    M, K, N, ld = 77, 512, 512, 576
+    a = rnd(M, K)
+    w = rnd(N, K, scale=0.05)
+    ar = Arena(M * ld * 2)
+    out = ar.view(BF, (M, N), strides=(ld, 1))
+    g = _gemm_args(a, w, out.data_ptr(), ld, L.EPI_HEADNORM, M, N, K, 100 + 10 * cfg + 1)
+    hw = (1 + 0.1 * torch.randn(2, 2, 128, device=DEV)).to(BF)
+    rope = torch.randn(M, 64, 2, device=DEV)
+    g.hn_w, g.hn_w_stride, g.hn_rope = hw.data_ptr(), 2 * 128, rope.data_ptr()
+    g.hn_heads, g.hn_nblk, g.hn_rope_heads, g.hn_seq_len, g.hn_pos0, g.hn_pos_mult, g.hn_eps = 2, 2, 2, M, 0, 1, 1e-6
+    wsb = lib().echo_gemm_ws_bytes(C.byref(g))
+    wa = Arena(max(wsb, 256))
+    ws = wa.view(torch.uint8, (max(wsb, 1),))
+    ok(lib().echo_gemm_ws(C.byref(g), ws.data_ptr(), wsb, stream()), "echo_gemm_ws")
+    ar.check(f"head-norm config {cfg} output")
+    wa.check(f"head-norm config {cfg} workspace")
+    assert torch.isfinite(out.float()).all()
+
+
 # ----------------------------------------------------------------------------------------- row-wise ops
 @pytest.mark.parametrize("rows_per_vec", [0, 13])
 def test_no_store_past_end_adaln(rows_per_vec):
