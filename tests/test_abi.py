@@ -225,7 +225,7 @@ def test_gemm_small_m_plan_host_policy(lib):
         return g
 
     ws = lambda M, N, K, epi=L.EPI_RESID: lib.echo_gemm_ws_bytes(C.byref(args(M, N, K, epi)))  # noqa: E731
-    assert ws(160, 2048, 5888) == 4 * 160 * 2048 * 4     # W2, one 160-latent block: config 5, 4 K splits
+    assert ws(160, 2048, 5888) == 4 * 160 * 2048 * 4     # W2, one 160-latent block: config 9, 4 K splits
     assert ws(480, 2048, 5888) == 4 * 480 * 2048 * 4     # CFG rows of a block: config 6, 4 splits
     assert ws(640, 2048, 5888) == 3 * 640 * 2048 * 4     # C2 plain step
     assert ws(160, 2048, 2048) == 2 * 160 * 2048 * 4     # Wo at 160 rows: 2 splits
@@ -240,9 +240,9 @@ def test_gemm_small_m_plan_host_policy(lib):
         assert lib.echo_set_policy_rows(1, 1) == 0
     assert ws(160, 2048, 5888) == 4 * 160 * 2048 * 4
     assert lib.echo_set_policy_rows(1, 2) != 0
-    # the planned launch (perf_model's labels): config 5 split 4 with a workspace, the best unsplit plan without
+    # the planned launch (perf_model's labels): config 9 split 4 with a workspace, the best unsplit plan without
     planned = lambda M, N, K, wsb, epi=L.EPI_RESID: lib.echo_gemm_planned_tile(C.byref(args(M, N, K, epi)), wsb)  # noqa: E731
-    assert planned(160, 2048, 5888, 4 * 160 * 2048 * 4) == 154
+    assert planned(160, 2048, 5888, 4 * 160 * 2048 * 4) == 194
     assert planned(480, 2048, 2048, 0) == 181           # config 8 unsplit, direct epilogue
     assert planned(30720, 2048, 5888, 0) == 20          # C3 W2: 320-row tiles (whole rounds)
     assert planned(1920, 11776, 2048, 0, L.EPI_SWIGLU) == 302  # C2 CFG W13: persistent 256x256 + small-M column split
