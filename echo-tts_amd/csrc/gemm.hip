@@ -738,7 +738,7 @@ gemm_bf16_sk_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __r
     if (NW >= 8 && !(abl & 32)) {
       if (!(abl & 1)) compute(lds + (kt % NS) * STAGE, more ? kt + NS - 1 : -1, (kt + NS - 1) % NS);
       else if (more) stage(kt + NS - 1, (kt + NS - 1) % NS);
-    } else {  // diag A/B (bit 32): the round-5 order, all of it between the barrier and the compute
+    } else {  // the 4-wave configs (and diag bit 32, A/B): all of it between the barrier and the compute
       if (more) stage(kt + NS - 1, (kt + NS - 1) % NS);
       if (!(abl & 1)) compute(lds + (kt % NS) * STAGE);
     }
